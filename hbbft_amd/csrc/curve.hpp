@@ -1,0 +1,300 @@
+// G1 / G2 group arithmetic for BLS12-381 on gfx950 (pairing 0.14.2 G1/G2, reference
+// Cargo.toml:28; used through threshold_crypto at honey_badger.rs:229/:340/:403 and
+// common_coin.rs:142/:151/:190).
+//
+// Points are Jacobian (X, Y, Z) with x = X/Z^2, y = Y/Z^3 in Montgomery form; Z = 0 is the
+// identity.  Affine points carry an explicit infinity flag.  Encodings follow the zcash format
+// pairing uses.
+#pragma once
+#include "field.hpp"
+
+namespace hbx {
+
+struct g1a {
+  fq x, y;
+  bool inf;
+};
+struct g1j {
+  fq x, y, z;
+};
+struct g2a {
+  fq2 x, y;
+  bool inf;
+};
+struct g2j {
+  fq2 x, y, z;
+};
+
+// Decode status codes (same values as include/hbx.h HBX_PT_*).
+#ifndef HBX_PT_OK
+#define HBX_PT_OK 0
+#define HBX_PT_BAD_FLAGS 1
+#define HBX_PT_NOT_IN_FIELD 2
+#define HBX_PT_NOT_ON_CURVE 3
+#define HBX_PT_INFINITY 4
+#endif
+
+// ----------------------------------------------------------------------------------------------
+// G1
+// ----------------------------------------------------------------------------------------------
+HBX_HD g1j g1_identity() { return g1j{fq_one(), fq_one(), fq_zero()}; }
+HBX_HD bool g1j_is_identity(const g1j& p) { return fq_is_zero(p.z); }
+HBX_HD g1j g1_from_affine(const g1a& a) {
+  if (a.inf) return g1_identity();
+  return g1j{a.x, a.y, fq_one()};
+}
+
+// dbl-2009-l (a = 0)
+HBX_HDNI g1j g1_dbl(const g1j& p) {
+  const fq A = fq_sqr(p.x);
+  const fq B = fq_sqr(p.y);
+  const fq C = fq_sqr(B);
+  fq D = fq_sub(fq_sub(fq_sqr(fq_add(p.x, B)), A), C);
+  D = fq_dbl(D);
+  const fq E = fq_add(fq_dbl(A), A);
+  const fq F = fq_sqr(E);
+  const fq X3 = fq_sub(F, fq_dbl(D));
+  const fq C8 = fq_dbl(fq_dbl(fq_dbl(C)));
+  const fq Y3 = fq_sub(fq_mul(E, fq_sub(D, X3)), C8);
+  const fq Z3 = fq_dbl(fq_mul(p.y, p.z));
+  return g1j{X3, Y3, Z3};
+}
+
+// add-2007-bl, complete for P == Q / P == -Q / identities.
+HBX_HDNI g1j g1_add(const g1j& p, const g1j& q) {
+  if (g1j_is_identity(p)) return q;
+  if (g1j_is_identity(q)) return p;
+  const fq Z1Z1 = fq_sqr(p.z);
+  const fq Z2Z2 = fq_sqr(q.z);
+  const fq U1 = fq_mul(p.x, Z2Z2);
+  const fq U2 = fq_mul(q.x, Z1Z1);
+  const fq S1 = fq_mul(fq_mul(p.y, q.z), Z2Z2);
+  const fq S2 = fq_mul(fq_mul(q.y, p.z), Z1Z1);
+  if (fq_eq(U1, U2)) {
+    if (fq_eq(S1, S2)) return g1_dbl(p);
+    return g1_identity();
+  }
+  const fq H = fq_sub(U2, U1);
+  const fq I = fq_sqr(fq_dbl(H));
+  const fq J = fq_mul(H, I);
+  const fq r = fq_dbl(fq_sub(S2, S1));
+  const fq V = fq_mul(U1, I);
+  const fq X3 = fq_sub(fq_sub(fq_sqr(r), J), fq_dbl(V));
+  const fq Y3 = fq_sub(fq_mul(r, fq_sub(V, X3)), fq_dbl(fq_mul(S1, J)));
+  const fq Z3 = fq_mul(fq_sub(fq_sub(fq_sqr(fq_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return g1j{X3, Y3, Z3};
+}
+
+HBX_HD g1j g1_neg(const g1j& p) { return g1j{p.x, fq_neg(p.y), p.z}; }
+
+HBX_HDNI g1a g1_to_affine(const g1j& p) {
+  g1a r;
+  if (g1j_is_identity(p)) {
+    r.x = fq_zero();
+    r.y = fq_zero();
+    r.inf = true;
+    return r;
+  }
+  const fq zi = fq_inv(p.z);
+  const fq zi2 = fq_sqr(zi);
+  r.x = fq_mul(p.x, zi2);
+  r.y = fq_mul(fq_mul(p.y, zi2), zi);
+  r.inf = false;
+  return r;
+}
+
+// 255-bit scalar (canonical, 8 limbs) times point, left-to-right double-and-add.
+HBX_HDNI g1j g1_mul_scalar(const g1j& p, const uint32_t* k8) {
+  g1j acc = g1_identity();
+  bool started = false;
+  for (int i = 255; i >= 0; i--) {
+    if (started) acc = g1_dbl(acc);
+    if ((k8[i >> 5] >> (i & 31)) & 1) {
+      acc = started ? g1_add(acc, p) : p;
+      started = true;
+    }
+  }
+  return acc;
+}
+
+// zcash compressed G1 -> affine (Montgomery).  No subgroup check.
+HBX_HDNI int32_t g1_decompress(const uint8_t* b48, g1a& out) {
+  const uint8_t flags = b48[0];
+  out.inf = false;
+  if (!(flags & 0x80)) return HBX_PT_BAD_FLAGS;
+  if (flags & 0x40) {
+    bool clean = !(flags & 0x20) && !(flags & 0x1F);
+    for (int i = 1; i < 48; i++) clean = clean && b48[i] == 0;
+    if (!clean) return HBX_PT_BAD_FLAGS;
+    out.x = fq_zero();
+    out.y = fq_zero();
+    out.inf = true;
+    return HBX_PT_INFINITY;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; i++) tmp[i] = b48[i];
+  tmp[0] &= 0x1F;
+  const fq xc = fq_from_be(tmp);
+  if (!fq_lt_p(xc)) return HBX_PT_NOT_IN_FIELD;
+  const fq x = fq_to_mont(xc);
+  const fq rhs = fq_add(fq_mul(fq_sqr(x), x), fq_from_const(FQ_B1));
+  fq y;
+  if (!fq_sqrt(rhs, y)) return HBX_PT_NOT_ON_CURVE;
+  if (fq_lex_largest(y) != ((flags & 0x20) != 0)) y = fq_neg(y);
+  out.x = x;
+  out.y = y;
+  return HBX_PT_OK;
+}
+
+HBX_HD void g1_compress(const g1a& p, uint8_t* b48) {
+  if (p.inf) {
+    for (int i = 0; i < 48; i++) b48[i] = 0;
+    b48[0] = 0xC0;
+    return;
+  }
+  fq_to_be(fq_from_mont(p.x), b48);
+  b48[0] |= 0x80;
+  if (fq_lex_largest(p.y)) b48[0] |= 0x20;
+}
+
+// ----------------------------------------------------------------------------------------------
+// G2 (twist y^2 = x^3 + 4(u+1))
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq2 g2_b() {
+  const fq four = fq_from_const(FQ_B1);
+  return fq2{four, four};
+}
+HBX_HD g2j g2_identity() { return g2j{fq2_one(), fq2_one(), fq2_zero()}; }
+HBX_HD bool g2j_is_identity(const g2j& p) { return fq2_is_zero(p.z); }
+HBX_HD g2j g2_from_affine(const g2a& a) {
+  if (a.inf) return g2_identity();
+  return g2j{a.x, a.y, fq2_one()};
+}
+
+HBX_HDNI g2j g2_dbl(const g2j& p) {
+  const fq2 A = fq2_sqr(p.x);
+  const fq2 B = fq2_sqr(p.y);
+  const fq2 C = fq2_sqr(B);
+  fq2 D = fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.x, B)), A), C);
+  D = fq2_dbl(D);
+  const fq2 E = fq2_add(fq2_dbl(A), A);
+  const fq2 F = fq2_sqr(E);
+  const fq2 X3 = fq2_sub(F, fq2_dbl(D));
+  const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
+  const fq2 Y3 = fq2_sub(fq2_mul(E, fq2_sub(D, X3)), C8);
+  const fq2 Z3 = fq2_dbl(fq2_mul(p.y, p.z));
+  return g2j{X3, Y3, Z3};
+}
+
+HBX_HDNI g2j g2_add(const g2j& p, const g2j& q) {
+  if (g2j_is_identity(p)) return q;
+  if (g2j_is_identity(q)) return p;
+  const fq2 Z1Z1 = fq2_sqr(p.z);
+  const fq2 Z2Z2 = fq2_sqr(q.z);
+  const fq2 U1 = fq2_mul(p.x, Z2Z2);
+  const fq2 U2 = fq2_mul(q.x, Z1Z1);
+  const fq2 S1 = fq2_mul(fq2_mul(p.y, q.z), Z2Z2);
+  const fq2 S2 = fq2_mul(fq2_mul(q.y, p.z), Z1Z1);
+  if (fq2_eq(U1, U2)) {
+    if (fq2_eq(S1, S2)) return g2_dbl(p);
+    return g2_identity();
+  }
+  const fq2 H = fq2_sub(U2, U1);
+  const fq2 I = fq2_sqr(fq2_dbl(H));
+  const fq2 J = fq2_mul(H, I);
+  const fq2 r = fq2_dbl(fq2_sub(S2, S1));
+  const fq2 V = fq2_mul(U1, I);
+  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr(r), J), fq2_dbl(V));
+  const fq2 Y3 = fq2_sub(fq2_mul(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul(S1, J)));
+  const fq2 Z3 = fq2_mul(fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return g2j{X3, Y3, Z3};
+}
+
+HBX_HD g2j g2_neg(const g2j& p) { return g2j{p.x, fq2_neg(p.y), p.z}; }
+
+HBX_HDNI g2a g2_to_affine(const g2j& p) {
+  g2a r;
+  if (g2j_is_identity(p)) {
+    r.x = fq2_zero();
+    r.y = fq2_zero();
+    r.inf = true;
+    return r;
+  }
+  const fq2 zi = fq2_inv(p.z);
+  const fq2 zi2 = fq2_sqr(zi);
+  r.x = fq2_mul(p.x, zi2);
+  r.y = fq2_mul(fq2_mul(p.y, zi2), zi);
+  r.inf = false;
+  return r;
+}
+
+// Scalar given as little-endian 32-bit limbs with an explicit bit length.
+HBX_HDNI g2j g2_mul_bits(const g2j& p, const uint32_t* k, int nbits) {
+  g2j acc = g2_identity();
+  bool started = false;
+  for (int i = nbits - 1; i >= 0; i--) {
+    if (started) acc = g2_dbl(acc);
+    if ((k[i >> 5] >> (i & 31)) & 1) {
+      acc = started ? g2_add(acc, p) : p;
+      started = true;
+    }
+  }
+  return acc;
+}
+
+// zcash compressed G2 (x.c1 || x.c0) -> affine (Montgomery).  No subgroup check.
+HBX_HDNI int32_t g2_decompress(const uint8_t* b96, g2a& out) {
+  const uint8_t flags = b96[0];
+  out.inf = false;
+  if (!(flags & 0x80)) return HBX_PT_BAD_FLAGS;
+  if (flags & 0x40) {
+    bool clean = !(flags & 0x20) && !(flags & 0x1F);
+    for (int i = 1; i < 96; i++) clean = clean && b96[i] == 0;
+    if (!clean) return HBX_PT_BAD_FLAGS;
+    out.x = fq2_zero();
+    out.y = fq2_zero();
+    out.inf = true;
+    return HBX_PT_INFINITY;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; i++) tmp[i] = b96[i];
+  tmp[0] &= 0x1F;
+  const fq x1c = fq_from_be(tmp);
+  const fq x0c = fq_from_be(b96 + 48);
+  if (!fq_lt_p(x1c) || !fq_lt_p(x0c)) return HBX_PT_NOT_IN_FIELD;
+  const fq2 x = fq2{fq_to_mont(x0c), fq_to_mont(x1c)};
+  const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+  fq2 y;
+  if (!fq2_sqrt(rhs, y)) return HBX_PT_NOT_ON_CURVE;
+  if (fq2_lex_largest(y) != ((flags & 0x20) != 0)) y = fq2_neg(y);
+  out.x = x;
+  out.y = y;
+  return HBX_PT_OK;
+}
+
+HBX_HD void g2_compress(const g2a& p, uint8_t* b96) {
+  if (p.inf) {
+    for (int i = 0; i < 96; i++) b96[i] = 0;
+    b96[0] = 0xC0;
+    return;
+  }
+  fq_to_be(fq_from_mont(p.x.c1), b96);
+  fq_to_be(fq_from_mont(p.x.c0), b96 + 48);
+  b96[0] |= 0x80;
+  if (fq2_lex_largest(p.y)) b96[0] |= 0x20;
+}
+
+// Uncompressed G2 (x.c1 || x.c0 || y.c1 || y.c0), as Signature::parity reads it.
+HBX_HD void g2_uncompressed(const g2a& p, uint8_t* b192) {
+  if (p.inf) {
+    for (int i = 0; i < 192; i++) b192[i] = 0;
+    b192[0] = 0x40;
+    return;
+  }
+  fq_to_be(fq_from_mont(p.x.c1), b192);
+  fq_to_be(fq_from_mont(p.x.c0), b192 + 48);
+  fq_to_be(fq_from_mont(p.y.c1), b192 + 96);
+  fq_to_be(fq_from_mont(p.y.c0), b192 + 144);
+}
+
+}  // namespace hbx

@@ -1,0 +1,648 @@
+// BLS12-381 base-field tower for gfx950: Fq (381-bit) / Fq2 / Fq6 / Fq12, and the scalar field Fr.
+//
+// What this replaces: the `pairing = 0.14.2` field types (reference Cargo.toml:28) that
+// threshold_crypto drives on hbbft's hot path.  The tower is the same
+// one pairing builds: Fq2 = Fq[u]/(u^2+1), Fq6 = Fq2[v]/(v^3-(u+1)), Fq12 = Fq6[w]/(w^2-v).
+//
+// Representation (MI355X-first):
+//  * 12 x 32-bit limbs, little-endian, Montgomery form with R = 2^384 (the same value pairing
+//    stores in 6 x u64).  Every multiply is a 12x12 CIOS loop of v_mad_u64_u32 (measured ~half
+//    rate on gfx950, tools/microbench/mad_rate.hip) -- integer VALU, not MFMA: this is not a
+//    dense contraction.
+//  * "Lazy" range [0, 2p]: p < 2^381 leaves 3 spare bits, so the no-carry CIOS takes inputs
+//    <= 2p and returns < 2p without a final subtraction (bounds checked numerically).  Add/sub
+//    fold back into [0, 2p) with one conditional 2p correction.  Canonical [0, p) form is only
+//    produced for encodings and equality tests (fq_canon).
+//  * Everything is __host__ __device__ so tools/hostcheck can unit-test the arithmetic on a CPU;
+//    the product path only ever runs it on the GPU.
+#pragma once
+#include <stdint.h>
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define HBX_HD __host__ __device__ __forceinline__
+#define HBX_HDNI __host__ __device__ __noinline__
+#else
+#define HBX_HD inline
+#define HBX_HDNI inline
+#endif
+#include "constants.hpp"
+
+namespace hbx {
+
+struct fq {
+  uint32_t l[12];
+};
+struct fq2 {
+  fq c0, c1;
+};
+struct fq6 {
+  fq2 c0, c1, c2;
+};
+struct fq12 {
+  fq6 c0, c1;
+};
+struct fr {
+  uint32_t l[8];
+};
+
+// ----------------------------------------------------------------------------------------------
+// Fq
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq fq_zero() {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = 0;
+  return r;
+}
+HBX_HD fq fq_one() {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = FQ_ONE[i];
+  return r;
+}
+HBX_HD fq fq_from_const(const uint32_t* c) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = c[i];
+  return r;
+}
+
+// Montgomery product, inputs <= 2p, output < 2p (no-carry CIOS; p's top limb < 2^31 - 1).
+// The outer (b-limb) loop is deliberately NOT unrolled: a fully unrolled product is ~900
+// instructions, and the Fq12 layers above would inline hundreds of them (multi-MB kernels that
+// thrash the 64 KB instruction cache and take hours to compile).  b's limbs rotate through a
+// register array so every index stays static (a dynamic b.l[i] is lowered to LDS traffic).
+HBX_HD fq fq_mul(const fq& a, const fq& b) {
+  uint32_t t[12], bb[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    t[j] = 0;
+    bb[j] = b.l[j];
+  }
+#pragma unroll 1
+  for (int i = 0; i < 12; i++) {
+    const uint32_t bi = bb[0];
+#pragma unroll
+    for (int k = 0; k < 11; k++) bb[k] = bb[k + 1];
+    uint64_t s = (uint64_t)a.l[0] * bi + t[0];
+    uint32_t A = (uint32_t)(s >> 32);
+    const uint32_t t0 = (uint32_t)s;
+    const uint32_t m = t0 * FQ_INV;
+    uint64_t c = (uint64_t)m * FQ_P[0] + t0;
+    uint32_t C = (uint32_t)(c >> 32);
+#pragma unroll
+    for (int j = 1; j < 12; j++) {
+      s = (uint64_t)a.l[j] * bi + t[j] + A;
+      A = (uint32_t)(s >> 32);
+      c = (uint64_t)m * FQ_P[j] + (uint32_t)s + C;
+      C = (uint32_t)(c >> 32);
+      t[j - 1] = (uint32_t)c;
+    }
+    t[11] = C + A;
+  }
+  fq r;
+#pragma unroll
+  for (int j = 0; j < 12; j++) r.l[j] = t[j];
+  return r;
+}
+
+HBX_HD fq fq_sqr(const fq& a) { return fq_mul(a, a); }
+
+// r = a + b reduced into [0, 2p) (inputs <= 2p).
+HBX_HD fq fq_add(const fq& a, const fq& b) {
+  fq s, d;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)a.l[i] + b.l[i] + carry;
+    s.l[i] = (uint32_t)v;
+    carry = v >> 32;
+  }
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)s.l[i] - FQ_2P[i] - borrow;
+    d.l[i] = (uint32_t)v;
+    borrow = (v >> 32) & 1;
+  }
+  // a + b < 4p < 2^384 so no carry out; keep s if s < 2p (borrow), else d
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = borrow ? s.l[i] : d.l[i];
+  return r;
+}
+
+// r = a - b (+2p if negative), result in [0, 2p].
+HBX_HD fq fq_sub(const fq& a, const fq& b) {
+  fq d;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)a.l[i] - b.l[i] - borrow;
+    d.l[i] = (uint32_t)v;
+    borrow = (v >> 32) & 1;
+  }
+  const uint32_t mask = 0u - (uint32_t)borrow;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)d.l[i] + (FQ_2P[i] & mask) + carry;
+    d.l[i] = (uint32_t)v;
+    carry = v >> 32;
+  }
+  return d;
+}
+
+HBX_HD fq fq_neg(const fq& a) { return fq_sub(fq_zero(), a); }
+HBX_HD fq fq_dbl(const fq& a) { return fq_add(a, a); }
+
+// Conditional subtract of a 12-limb constant if x >= c.
+HBX_HD fq fq_csub(const fq& x, const uint32_t* c) {
+  fq d;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)x.l[i] - c[i] - borrow;
+    d.l[i] = (uint32_t)v;
+    borrow = (v >> 32) & 1;
+  }
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = borrow ? x.l[i] : d.l[i];
+  return r;
+}
+
+// Canonical representative in [0, p) of a lazy value in [0, 2p].
+HBX_HD fq fq_canon(const fq& a) { return fq_csub(fq_csub(a, FQ_P), FQ_P); }
+
+HBX_HD bool fq_is_zero(const fq& a) {
+  fq c = fq_canon(a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o |= c.l[i];
+  return o == 0;
+}
+HBX_HD bool fq_eq(const fq& a, const fq& b) { return fq_is_zero(fq_sub(a, b)); }
+
+HBX_HD fq fq_to_mont(const fq& a) { return fq_mul(a, fq_from_const(FQ_R2)); }
+HBX_HD fq fq_from_mont(const fq& a) {
+  fq one = fq_zero();
+  one.l[0] = 1;
+  return fq_canon(fq_mul(a, one));
+}
+
+// a^e for a fixed 12-limb exponent, left-to-right, 4-bit fixed window (~381 S + ~95 M).
+HBX_HDNI fq fq_pow_const(const fq& a, const uint32_t* e) {
+  fq tab[16];
+  tab[0] = fq_one();
+  tab[1] = a;
+  for (int i = 2; i < 16; i++) tab[i] = fq_mul(tab[i - 1], a);
+  fq r = fq_one();
+  bool started = false;
+  for (int w = 95; w >= 0; w--) {
+    const uint32_t nib = (e[w >> 3] >> ((w & 7) * 4)) & 0xF;
+    if (started) {
+      r = fq_sqr(r);
+      r = fq_sqr(r);
+      r = fq_sqr(r);
+      r = fq_sqr(r);
+    }
+    if (nib) {
+      // select tab[nib] without dynamic register indexing
+      fq t = tab[1];
+      for (int k = 2; k < 16; k++)
+        if ((uint32_t)k == nib) t = tab[k];
+      r = started ? fq_mul(r, t) : t;
+      started = true;
+    }
+  }
+  return r;
+}
+
+HBX_HD fq fq_inv(const fq& a) { return fq_pow_const(a, FQ_P_MINUS_2); }
+
+// Square root for p = 3 mod 4.  Returns false if a is a non-residue.
+HBX_HD bool fq_sqrt(const fq& a, fq& out) {
+  fq s = fq_pow_const(a, FQ_SQRT_EXP);
+  out = s;
+  return fq_eq(fq_sqr(s), a);
+}
+
+// Lexicographic "largest" flag of the zcash encoding: canonical(y) > (p-1)/2.
+HBX_HD bool fq_lex_largest(const fq& y_mont) {
+  fq y = fq_from_mont(y_mont);
+  // y > (p-1)/2  <=>  (p-1)/2 - y borrows
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)FQ_P_MINUS_1_HALF[i] - y.l[i] - borrow;
+    borrow = (v >> 32) & 1;
+  }
+  return borrow != 0;
+}
+
+// Big-endian 48-byte encoding <-> canonical limbs (not Montgomery).
+HBX_HD fq fq_from_be(const uint8_t* b) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  return r;
+}
+HBX_HD void fq_to_be(const fq& a, uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.l[i] >> 24);
+    q[1] = (uint8_t)(a.l[i] >> 16);
+    q[2] = (uint8_t)(a.l[i] >> 8);
+    q[3] = (uint8_t)a.l[i];
+  }
+}
+// true iff canonical value < p
+HBX_HD bool fq_lt_p(const fq& a) {
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t v = (uint64_t)a.l[i] - FQ_P[i] - borrow;
+    borrow = (v >> 32) & 1;
+  }
+  return borrow != 0;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fq2 = Fq[u]/(u^2 + 1)
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq2 fq2_zero() { return fq2{fq_zero(), fq_zero()}; }
+HBX_HD fq2 fq2_one() { return fq2{fq_one(), fq_zero()}; }
+HBX_HD fq2 fq2_add(const fq2& a, const fq2& b) { return fq2{fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)}; }
+HBX_HD fq2 fq2_sub(const fq2& a, const fq2& b) { return fq2{fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)}; }
+HBX_HD fq2 fq2_neg(const fq2& a) { return fq2{fq_neg(a.c0), fq_neg(a.c1)}; }
+HBX_HD fq2 fq2_dbl(const fq2& a) { return fq2{fq_dbl(a.c0), fq_dbl(a.c1)}; }
+HBX_HD fq2 fq2_conj(const fq2& a) { return fq2{a.c0, fq_neg(a.c1)}; }
+
+HBX_HD fq2 fq2_mul(const fq2& a, const fq2& b) {
+  const fq t0 = fq_mul(a.c0, b.c0);
+  const fq t1 = fq_mul(a.c1, b.c1);
+  const fq t2 = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
+  return fq2{fq_sub(t0, t1), fq_sub(fq_sub(t2, t0), t1)};
+}
+HBX_HD fq2 fq2_sqr(const fq2& a) {
+  // (a0 + a1)(a0 - a1), 2 a0 a1
+  const fq t0 = fq_mul(fq_add(a.c0, a.c1), fq_sub(a.c0, a.c1));
+  const fq t1 = fq_mul(a.c0, a.c1);
+  return fq2{t0, fq_dbl(t1)};
+}
+HBX_HD fq2 fq2_mul_fq(const fq2& a, const fq& s) { return fq2{fq_mul(a.c0, s), fq_mul(a.c1, s)}; }
+// multiply by the Fq6 non-residue xi = 1 + u
+HBX_HD fq2 fq2_mul_xi(const fq2& a) { return fq2{fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1)}; }
+HBX_HD bool fq2_is_zero(const fq2& a) { return fq_is_zero(a.c0) && fq_is_zero(a.c1); }
+HBX_HD bool fq2_eq(const fq2& a, const fq2& b) { return fq_eq(a.c0, b.c0) && fq_eq(a.c1, b.c1); }
+HBX_HD fq2 fq2_canon(const fq2& a) { return fq2{fq_canon(a.c0), fq_canon(a.c1)}; }
+
+HBX_HDNI fq2 fq2_inv(const fq2& a) {
+  const fq n = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+  const fq ni = fq_inv(n);
+  return fq2{fq_mul(a.c0, ni), fq_neg(fq_mul(a.c1, ni))};
+}
+
+// pairing 0.14 Ord on Fq2 (c1 first, then c0) applied to (y, -y): is y the larger root?
+HBX_HD int fq_cmp_canon(const fq& a, const fq& b) {  // canonical inputs
+  for (int i = 11; i >= 0; i--) {
+    if (a.l[i] != b.l[i]) return a.l[i] > b.l[i] ? 1 : -1;
+  }
+  return 0;
+}
+HBX_HD bool fq2_lex_largest(const fq2& y_mont) {
+  const fq y0 = fq_from_mont(y_mont.c0), y1 = fq_from_mont(y_mont.c1);
+  const fq2 n = fq2_neg(y_mont);
+  const fq n0 = fq_from_mont(n.c0), n1 = fq_from_mont(n.c1);
+  int c = fq_cmp_canon(y1, n1);
+  if (c == 0) c = fq_cmp_canon(y0, n0);
+  return c > 0;
+}
+
+// Fq2 square root (p = 3 mod 4), "complex method".  Returns false for a non-residue.
+HBX_HDNI bool fq2_sqrt(const fq2& a, fq2& out) {
+  if (fq_is_zero(a.c1)) {
+    fq s;
+    if (fq_sqrt(a.c0, s)) {
+      out = fq2{s, fq_zero()};
+      return true;
+    }
+    if (fq_sqrt(fq_neg(a.c0), s)) {
+      out = fq2{fq_zero(), s};
+      return true;
+    }
+    return false;
+  }
+  fq alpha;
+  if (!fq_sqrt(fq_add(fq_sqr(a.c0), fq_sqr(a.c1)), alpha)) return false;
+  // inverse of 2 in Montgomery form: (p+1)/2 * R
+  fq two = fq_dbl(fq_one());
+  fq inv2 = fq_inv(two);
+  fq delta = fq_mul(fq_add(a.c0, alpha), inv2);
+  fq x0;
+  if (!fq_sqrt(delta, x0)) {
+    delta = fq_mul(fq_sub(a.c0, alpha), inv2);
+    if (!fq_sqrt(delta, x0)) return false;
+  }
+  fq x1 = fq_mul(a.c1, fq_inv(fq_dbl(x0)));
+  out = fq2{x0, x1};
+  return fq2_eq(fq2_sqr(out), a);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fq6 = Fq2[v]/(v^3 - xi)
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq6 fq6_zero() { return fq6{fq2_zero(), fq2_zero(), fq2_zero()}; }
+HBX_HD fq6 fq6_one() { return fq6{fq2_one(), fq2_zero(), fq2_zero()}; }
+HBX_HD fq6 fq6_add(const fq6& a, const fq6& b) {
+  return fq6{fq2_add(a.c0, b.c0), fq2_add(a.c1, b.c1), fq2_add(a.c2, b.c2)};
+}
+HBX_HD fq6 fq6_sub(const fq6& a, const fq6& b) {
+  return fq6{fq2_sub(a.c0, b.c0), fq2_sub(a.c1, b.c1), fq2_sub(a.c2, b.c2)};
+}
+HBX_HD fq6 fq6_neg(const fq6& a) { return fq6{fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)}; }
+// multiply by v: (c0, c1, c2) v = (xi c2, c0, c1)
+HBX_HD fq6 fq6_mul_v(const fq6& a) { return fq6{fq2_mul_xi(a.c2), a.c0, a.c1}; }
+
+// Karatsuba-style Fq6 product (6 Fq2 mults).
+HBX_HDNI fq6 fq6_mul(const fq6& a, const fq6& b) {
+  const fq2 t0 = fq2_mul(a.c0, b.c0);
+  const fq2 t1 = fq2_mul(a.c1, b.c1);
+  const fq2 t2 = fq2_mul(a.c2, b.c2);
+  // c0 = t0 + xi((a1+a2)(b1+b2) - t1 - t2)
+  fq2 c0 = fq2_mul(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2));
+  c0 = fq2_add(t0, fq2_mul_xi(fq2_sub(fq2_sub(c0, t1), t2)));
+  // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
+  fq2 c1 = fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1));
+  c1 = fq2_add(fq2_sub(fq2_sub(c1, t0), t1), fq2_mul_xi(t2));
+  // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
+  fq2 c2 = fq2_mul(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2));
+  c2 = fq2_add(fq2_sub(fq2_sub(c2, t0), t2), t1);
+  return fq6{c0, c1, c2};
+}
+
+HBX_HDNI fq6 fq6_sqr(const fq6& a) {
+  // CH-SQR2
+  const fq2 s0 = fq2_sqr(a.c0);
+  const fq2 ab = fq2_mul(a.c0, a.c1);
+  const fq2 s1 = fq2_dbl(ab);
+  const fq2 s2 = fq2_sqr(fq2_add(fq2_sub(a.c0, a.c1), a.c2));
+  const fq2 bc = fq2_mul(a.c1, a.c2);
+  const fq2 s3 = fq2_dbl(bc);
+  const fq2 s4 = fq2_sqr(a.c2);
+  const fq2 c0 = fq2_add(s0, fq2_mul_xi(s3));
+  const fq2 c1 = fq2_add(s1, fq2_mul_xi(s4));
+  const fq2 c2 = fq2_sub(fq2_sub(fq2_add(fq2_add(s1, s2), s3), s0), s4);
+  return fq6{c0, c1, c2};
+}
+
+// a * (b0 + b1 v)   (5 Fq2 mults)
+HBX_HDNI fq6 fq6_mul_by_01(const fq6& a, const fq2& b0, const fq2& b1) {
+  const fq2 t0 = fq2_mul(a.c0, b0);
+  const fq2 t1 = fq2_mul(a.c1, b1);
+  // c0 = t0 + xi * (a2 * b1)
+  const fq2 c0 = fq2_add(t0, fq2_mul_xi(fq2_mul(a.c2, b1)));
+  // c1 = (a0 + a1)(b0 + b1) - t0 - t1
+  const fq2 c1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b0, b1)), t0), t1);
+  // c2 = a2 * b0 + t1
+  const fq2 c2 = fq2_add(fq2_mul(a.c2, b0), t1);
+  return fq6{c0, c1, c2};
+}
+
+// a * (s v) with s in Fq: (xi a2 s, a0 s, a1 s)
+HBX_HD fq6 fq6_mul_by_1_fq(const fq6& a, const fq& s) {
+  return fq6{fq2_mul_xi(fq2_mul_fq(a.c2, s)), fq2_mul_fq(a.c0, s), fq2_mul_fq(a.c1, s)};
+}
+
+HBX_HDNI fq6 fq6_inv(const fq6& a) {
+  const fq2 c0 = fq2_sub(fq2_sqr(a.c0), fq2_mul_xi(fq2_mul(a.c1, a.c2)));
+  const fq2 c1 = fq2_sub(fq2_mul_xi(fq2_sqr(a.c2)), fq2_mul(a.c0, a.c1));
+  const fq2 c2 = fq2_sub(fq2_sqr(a.c1), fq2_mul(a.c0, a.c2));
+  const fq2 t = fq2_add(fq2_mul(a.c0, c0), fq2_mul_xi(fq2_add(fq2_mul(a.c2, c1), fq2_mul(a.c1, c2))));
+  const fq2 ti = fq2_inv(t);
+  return fq6{fq2_mul(c0, ti), fq2_mul(c1, ti), fq2_mul(c2, ti)};
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fq12 = Fq6[w]/(w^2 - v)
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq12 fq12_one() { return fq12{fq6_one(), fq6_zero()}; }
+HBX_HD fq12 fq12_conj(const fq12& a) { return fq12{a.c0, fq6_neg(a.c1)}; }
+
+HBX_HDNI fq12 fq12_mul(const fq12& a, const fq12& b) {
+  const fq6 t0 = fq6_mul(a.c0, b.c0);
+  const fq6 t1 = fq6_mul(a.c1, b.c1);
+  const fq6 c1 = fq6_sub(fq6_sub(fq6_mul(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1)), t0), t1);
+  return fq12{fq6_add(t0, fq6_mul_v(t1)), c1};
+}
+
+HBX_HDNI fq12 fq12_sqr(const fq12& a) {
+  // complex squaring: c0 = (a0 + a1)(a0 + v a1) - ab - v ab, c1 = 2 ab
+  const fq6 ab = fq6_mul(a.c0, a.c1);
+  const fq6 t = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));
+  const fq6 c0 = fq6_sub(fq6_sub(t, ab), fq6_mul_v(ab));
+  return fq12{c0, fq6_add(ab, ab)};
+}
+
+// f * (c0 + c1 v + c4 v w) with c0, c1 in Fq2 and c4 in Fq -- the shape of a prepared line
+// evaluated at a G1 point (pairing's mul_by_014, with c4 real).
+HBX_HDNI fq12 fq12_mul_by_014(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
+  const fq6 aa = fq6_mul_by_01(f.c0, c0, c1);
+  const fq6 bb = fq6_mul_by_1_fq(f.c1, c4);
+  const fq2 o = fq2{fq_add(c1.c0, c4), c1.c1};
+  fq6 s = fq6_add(f.c1, f.c0);
+  s = fq6_mul_by_01(s, c0, o);
+  const fq6 n1 = fq6_sub(fq6_sub(s, aa), bb);
+  const fq6 n0 = fq6_add(fq6_mul_v(bb), aa);
+  return fq12{n0, n1};
+}
+
+HBX_HDNI fq12 fq12_inv(const fq12& a) {
+  const fq6 t = fq6_sub(fq6_sqr(a.c0), fq6_mul_v(fq6_sqr(a.c1)));
+  const fq6 ti = fq6_inv(t);
+  return fq12{fq6_mul(a.c0, ti), fq6_neg(fq6_mul(a.c1, ti))};
+}
+
+// Frobenius maps.  With f = sum g_i w^i (g0..g5 = c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2),
+// (g w^i)^p = conj(g) gamma_1,i w^i and (g w^i)^(p^2) = g gamma_2,i w^i.
+HBX_HD fq2 fq2_frob_coef1(const fq2& g, int i) {
+  const uint32_t* k0 = i == 1 ? FROB1_C1_0 : i == 2 ? FROB1_C2_0 : i == 3 ? FROB1_C3_0 : i == 4 ? FROB1_C4_0 : FROB1_C5_0;
+  const uint32_t* k1 = i == 1 ? FROB1_C1_1 : i == 2 ? FROB1_C2_1 : i == 3 ? FROB1_C3_1 : i == 4 ? FROB1_C4_1 : FROB1_C5_1;
+  return fq2_mul(fq2_conj(g), fq2{fq_from_const(k0), fq_from_const(k1)});
+}
+HBX_HDNI fq12 fq12_frobenius(const fq12& a) {
+  fq12 r;
+  r.c0.c0 = fq2_conj(a.c0.c0);
+  r.c1.c0 = fq2_frob_coef1(a.c1.c0, 1);
+  r.c0.c1 = fq2_frob_coef1(a.c0.c1, 2);
+  r.c1.c1 = fq2_frob_coef1(a.c1.c1, 3);
+  r.c0.c2 = fq2_frob_coef1(a.c0.c2, 4);
+  r.c1.c2 = fq2_frob_coef1(a.c1.c2, 5);
+  return r;
+}
+HBX_HDNI fq12 fq12_frobenius2(const fq12& a) {
+  fq12 r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fq2_mul_fq(a.c1.c0, fq_from_const(FROB2_C1));
+  r.c0.c1 = fq2_mul_fq(a.c0.c1, fq_from_const(FROB2_C2));
+  r.c1.c1 = fq2_mul_fq(a.c1.c1, fq_from_const(FROB2_C3));
+  r.c0.c2 = fq2_mul_fq(a.c0.c2, fq_from_const(FROB2_C4));
+  r.c1.c2 = fq2_mul_fq(a.c1.c2, fq_from_const(FROB2_C5));
+  return r;
+}
+
+// Granger-Scott squaring, valid in the cyclotomic subgroup (after the easy part).
+HBX_HD void fq4_sqr(const fq2& a, const fq2& b, fq2& c0, fq2& c1) {
+  const fq2 t0 = fq2_sqr(a);
+  const fq2 t1 = fq2_sqr(b);
+  c0 = fq2_add(fq2_mul_xi(t1), t0);
+  c1 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(a, b)), t0), t1);
+}
+HBX_HDNI fq12 fq12_cyclotomic_sqr(const fq12& f) {
+  fq2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
+  fq2 z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fq2 t0, t1, t2, t3;
+  fq4_sqr(z0, z1, t0, t1);
+  z0 = fq2_sub(t0, z0);
+  z0 = fq2_add(fq2_dbl(z0), t0);
+  z1 = fq2_add(t1, z1);
+  z1 = fq2_add(fq2_dbl(z1), t1);
+  fq4_sqr(z2, z3, t0, t1);
+  fq4_sqr(z4, z5, t2, t3);
+  z4 = fq2_sub(t0, z4);
+  z4 = fq2_add(fq2_dbl(z4), t0);
+  z5 = fq2_add(t1, z5);
+  z5 = fq2_add(fq2_dbl(z5), t1);
+  t0 = fq2_mul_xi(t3);
+  z2 = fq2_add(t0, z2);
+  z2 = fq2_add(fq2_dbl(z2), t0);
+  z3 = fq2_sub(t2, z3);
+  z3 = fq2_add(fq2_dbl(z3), t2);
+  return fq12{fq6{z0, z4, z3}, fq6{z2, z1, z5}};
+}
+
+HBX_HD bool fq12_is_one(const fq12& a) {
+  const fq12 o = fq12_one();
+  return fq2_eq(a.c0.c0, o.c0.c0) && fq2_is_zero(a.c0.c1) && fq2_is_zero(a.c0.c2) &&
+         fq2_is_zero(a.c1.c0) && fq2_is_zero(a.c1.c1) && fq2_is_zero(a.c1.c2);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fr (255-bit scalar field): 8 limbs, Montgomery R = 2^256, canonical outputs (< r).
+// ----------------------------------------------------------------------------------------------
+HBX_HD fr fr_from_const(const uint32_t* c) {
+  fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = c[i];
+  return r;
+}
+HBX_HD fr fr_csub(const fr& x) {
+  fr d;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = (uint64_t)x.l[i] - FR_R[i] - borrow;
+    d.l[i] = (uint32_t)v;
+    borrow = (v >> 32) & 1;
+  }
+  fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = borrow ? x.l[i] : d.l[i];
+  return r;
+}
+// Montgomery product with a full carry word (r's top limb is large: no lazy trick), output < r.
+HBX_HDNI fr fr_mul(const fr& a, const fr& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c = (uint64_t)a.l[j] * b.l[i] + t[j] + (c >> 32);
+      t[j] = (uint32_t)c;
+    }
+    uint64_t s = (uint64_t)t[8] + (c >> 32);
+    t[8] = (uint32_t)s;
+    t[9] = (uint32_t)(s >> 32);
+    const uint32_t m = t[0] * FR_INV;
+    c = (uint64_t)m * FR_R[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      c = (uint64_t)m * FR_R[j] + t[j] + (c >> 32);
+      t[j - 1] = (uint32_t)c;
+    }
+    s = (uint64_t)t[8] + (c >> 32);
+    t[7] = (uint32_t)s;
+    t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  fr r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.l[j] = t[j];
+  // t < 2r; t[8] may hold the top carry
+  if (t[8]) {
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t v = (uint64_t)r.l[i] - FR_R[i] - borrow;
+      r.l[i] = (uint32_t)v;
+      borrow = (v >> 32) & 1;
+    }
+    return r;
+  }
+  return fr_csub(r);
+}
+HBX_HD fr fr_add(const fr& a, const fr& b) {
+  fr s;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c = (uint64_t)a.l[i] + b.l[i] + (c >> 32);
+    s.l[i] = (uint32_t)c;
+  }
+  return fr_csub(s);  // a + b < 2r < 2^256
+}
+HBX_HD fr fr_sub(const fr& a, const fr& b) {
+  fr d;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = (uint64_t)a.l[i] - b.l[i] - borrow;
+    d.l[i] = (uint32_t)v;
+    borrow = (v >> 32) & 1;
+  }
+  if (borrow) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c = (uint64_t)d.l[i] + FR_R[i] + (c >> 32);
+      d.l[i] = (uint32_t)c;
+    }
+  }
+  return d;
+}
+HBX_HD fr fr_to_mont(const fr& a) { return fr_mul(a, fr_from_const(FR_R2)); }
+HBX_HD fr fr_from_mont(const fr& a) {
+  fr one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.l[i] = 0;
+  one.l[0] = 1;
+  return fr_mul(a, one);
+}
+HBX_HDNI fr fr_pow_const(const fr& a, const uint32_t* e) {
+  fr r = fr_from_const(FR_ONE);
+  for (int i = 255; i >= 0; i--) {
+    r = fr_mul(r, r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = fr_mul(r, a);
+  }
+  return r;
+}
+HBX_HD fr fr_inv(const fr& a) { return fr_pow_const(a, FR_R_MINUS_2); }
+
+}  // namespace hbx

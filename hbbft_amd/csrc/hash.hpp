@@ -1,0 +1,215 @@
+// Byte-level primitives on the hot path:
+//  * SHA-256 (FIPS 180-4) -- the digest threshold_crypto applies inside hash_g2 / hash_g1_g2 /
+//    hash_bytes (DIGEST default = SHA-256, the reference's own `ring`
+//    dependency, Cargo.toml:32) and the Merkle hash of broadcast.rs:381/:683;
+//  * ChaCha20 as `rand 0.4` ChaChaRng emits it (Cargo.toml:29): key = 8 seed words, 128-bit
+//    block counter in words 12..15, words returned in block order, next_u64 = hi<<32 | lo;
+//  * hash_g2 / hash_g1_g2 (threshold_crypto): digest -> 8 big-endian seed words -> ChaChaRng ->
+//    pairing 0.14 `G2::rand` (Fq2 sampled in raw Montgomery representation, bool `greatest`,
+//    lift, multiply by the full cofactor h2, retry).
+#pragma once
+#include "curve.hpp"
+
+namespace hbx {
+
+// ----------------------------------------------------------------------------------------------
+// SHA-256
+// ----------------------------------------------------------------------------------------------
+HBX_CONST uint32_t SHA256_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+HBX_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+HBX_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+struct sha256_state {
+  uint32_t h[8];
+};
+
+HBX_HD void sha256_init(sha256_state& s) {
+  s.h[0] = 0x6a09e667u; s.h[1] = 0xbb67ae85u; s.h[2] = 0x3c6ef372u; s.h[3] = 0xa54ff53au;
+  s.h[4] = 0x510e527fu; s.h[5] = 0x9b05688cu; s.h[6] = 0x1f83d9abu; s.h[7] = 0x5be0cd19u;
+}
+
+// One compression over 16 big-endian message words.
+HBX_HDNI void sha256_compress(sha256_state& s, const uint32_t* w16) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = w16[i];
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+  s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+// Streaming SHA-256 over a concatenation of up to two byte ranges (enough for hash_g1_g2's
+// "message || compress(g1)"), one lane.  Output: 32-byte digest.
+HBX_HD void sha256_2(const uint8_t* m0, uint64_t n0, const uint8_t* m1, uint64_t n1, uint8_t* out32) {
+  sha256_state s;
+  sha256_init(s);
+  const uint64_t total = n0 + n1;
+  const uint64_t nblocks = (total + 9 + 63) / 64;
+  for (uint64_t blk = 0; blk < nblocks; blk++) {
+    uint32_t w[16];
+    for (int i = 0; i < 16; i++) {
+      uint32_t word = 0;
+      for (int k = 0; k < 4; k++) {
+        const uint64_t pos = blk * 64 + (uint64_t)(4 * i + k);
+        uint8_t byte;
+        if (pos < n0) byte = m0[pos];
+        else if (pos < total) byte = m1[pos - n0];
+        else if (pos == total) byte = 0x80;
+        else if (pos >= nblocks * 64 - 8) byte = (uint8_t)((total * 8) >> (8 * (nblocks * 64 - 1 - pos)));
+        else byte = 0;
+        word = (word << 8) | byte;
+      }
+      w[i] = word;
+    }
+    sha256_compress(s, w);
+  }
+  for (int i = 0; i < 8; i++) {
+    out32[4 * i] = (uint8_t)(s.h[i] >> 24);
+    out32[4 * i + 1] = (uint8_t)(s.h[i] >> 16);
+    out32[4 * i + 2] = (uint8_t)(s.h[i] >> 8);
+    out32[4 * i + 3] = (uint8_t)s.h[i];
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// ChaCha20 / rand 0.4 ChaChaRng
+// ----------------------------------------------------------------------------------------------
+#define HBX_QR(a, b, c, d)       \
+  a += b; d = rotl32(d ^ a, 16); \
+  c += d; b = rotl32(b ^ c, 12); \
+  a += b; d = rotl32(d ^ a, 8);  \
+  c += d; b = rotl32(b ^ c, 7);
+
+// One 16-word output block for key words k[8] and 128-bit counter (ctr_lo, ctr_hi).
+HBX_HDNI void chacha20_block(const uint32_t* k, uint64_t ctr_lo, uint64_t ctr_hi, uint32_t* out16) {
+  uint32_t st[16] = {0x61707865u, 0x3320646Eu, 0x79622D32u, 0x6B206574u, k[0], k[1], k[2], k[3],
+                     k[4], k[5], k[6], k[7], (uint32_t)ctr_lo, (uint32_t)(ctr_lo >> 32),
+                     (uint32_t)ctr_hi, (uint32_t)(ctr_hi >> 32)};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = st[i];
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    HBX_QR(x[0], x[4], x[8], x[12]);
+    HBX_QR(x[1], x[5], x[9], x[13]);
+    HBX_QR(x[2], x[6], x[10], x[14]);
+    HBX_QR(x[3], x[7], x[11], x[15]);
+    HBX_QR(x[0], x[5], x[10], x[15]);
+    HBX_QR(x[1], x[6], x[11], x[12]);
+    HBX_QR(x[2], x[7], x[8], x[13]);
+    HBX_QR(x[3], x[4], x[9], x[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) out16[i] = x[i] + st[i];
+}
+
+struct chacha_rng {
+  uint32_t key[8];
+  uint32_t buf[16];
+  uint64_t ctr;  // next block number (low 64 bits of the 128-bit counter suffice here)
+  int idx;
+};
+
+HBX_HD void chacha_rng_from_digest(chacha_rng& r, const uint8_t* d32) {
+  for (int i = 0; i < 8; i++)
+    r.key[i] = ((uint32_t)d32[4 * i] << 24) | ((uint32_t)d32[4 * i + 1] << 16) |
+               ((uint32_t)d32[4 * i + 2] << 8) | d32[4 * i + 3];
+  r.ctr = 0;
+  r.idx = 16;
+}
+HBX_HD uint32_t chacha_next_u32(chacha_rng& r) {
+  if (r.idx == 16) {
+    chacha20_block(r.key, r.ctr, 0, r.buf);
+    r.ctr++;
+    r.idx = 0;
+  }
+  return r.buf[r.idx++];
+}
+HBX_HD uint64_t chacha_next_u64(chacha_rng& r) {
+  const uint64_t hi = chacha_next_u32(r);
+  const uint64_t lo = chacha_next_u32(r);
+  return (hi << 32) | lo;
+}
+
+// pairing 0.14 `Fq::rand`: 6 x next_u64 limbs, top limb masked to 61 bits, rejection-sampled,
+// the raw limbs ARE the Montgomery representation.
+HBX_HD fq fq_rand(chacha_rng& r) {
+  for (;;) {
+    fq v;
+    for (int i = 0; i < 6; i++) {
+      const uint64_t w = chacha_next_u64(r);
+      v.l[2 * i] = (uint32_t)w;
+      v.l[2 * i + 1] = (uint32_t)(w >> 32);
+    }
+    v.l[11] &= 0x1FFFFFFFu;
+    if (fq_lt_p(v)) return v;
+  }
+}
+
+// G2::rand + scale_by_cofactor (full h2).
+HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
+  for (;;) {
+    const fq c0 = fq_rand(r);
+    const fq c1 = fq_rand(r);
+    const fq2 x = fq2{c0, c1};
+    const bool greatest = (chacha_next_u32(r) & 1u) != 0;
+    const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+    fq2 y;
+    if (!fq2_sqrt(rhs, y)) continue;
+    // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
+    if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
+    const g2j p = g2_mul_bits(g2j{x, y, fq2_one()}, G2_COFACTOR, G2_COFACTOR_BITS);
+    if (!g2j_is_identity(p)) return p;
+  }
+}
+
+// hash_g2(digest) where the digest is already computed.
+HBX_HD g2j hash_g2_from_digest(const uint8_t* d32) {
+  chacha_rng r;
+  chacha_rng_from_digest(r, d32);
+  return g2_rand_from_rng(r);
+}
+
+// hash_g1_g2(u, v): m = (|v| > 64 ? SHA256(v) : v) || u_comp48; H = hash_g2(m).
+HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen) {
+  uint8_t d[32];
+  if (vlen > 64) {
+    uint8_t dv[32];
+    sha256_2(v, vlen, nullptr, 0, dv);
+    sha256_2(dv, 32, u_comp48, 48, d);
+  } else {
+    sha256_2(v, vlen, u_comp48, 48, d);
+  }
+  return hash_g2_from_digest(d);
+}
+
+}  // namespace hbx

@@ -1,0 +1,293 @@
+// C-ABI implementation (include/hbx.h): context, device buffers, kernel launches.
+// Host code only orchestrates -- every verification, combine and hash runs in the HIP kernels of
+// hbx_kernels.hip.  There is no CPU fallback: without a usable HIP device every call fails with
+// HBX_E_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hbx.h"
+#include "hbx_kernels.hip"
+
+using namespace hbx;
+
+namespace {
+
+struct dbuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(&p, bytes) != hipSuccess) return false;
+    cap = bytes;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct hbx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err = "ok";
+  // era state
+  uint32_t n_keys = 0;
+  dbuf pk, pk_status, pk_comp;
+  // epoch state
+  uint32_t p_ct = 0;
+  dbuf U, G2pts, lines, scratch, ct_ok, ct_valid;
+  const uint8_t* d_v_blob = nullptr;  // device V blob used by the combine (caller-owned for _d)
+  const uint64_t* d_v_off = nullptr;
+  uint64_t max_v_len = 0;
+  dbuf v_blob_own, v_off_own, u_comp_own, w_comp_own;
+  // verification state
+  uint32_t n_shares = 0;
+  dbuf S, valid, shares_own, present_own;
+  // combine state
+  dbuf keys, status, out_own;
+};
+
+static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                      \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail(ctx, HBX_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static hipStream_t pick(hbx_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+
+static void pack_bits(const uint8_t* bytes, size_t n, uint8_t* bits) {
+  memset(bits, 0, (n + 7) / 8);
+  for (size_t k = 0; k < n; k++)
+    if (bytes[k]) bits[k >> 3] |= (uint8_t)(1u << (k & 7));
+}
+
+extern "C" {
+
+const char* hbx_version(void) { return "hbx 0.1.0 gfx950"; }
+
+const char* hbx_last_error(const hbx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int hbx_ctx_create(int device, hbx_ctx** out) {
+  if (!out) return HBX_E_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return HBX_E_DEVICE;
+  if (device < 0 || device >= count) return HBX_E_INVALID_ARG;
+  if (hipSetDevice(device) != hipSuccess) return HBX_E_DEVICE;
+  hbx_ctx* c = new hbx_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HBX_E_DEVICE;
+  }
+  *out = c;
+  return HBX_OK;
+}
+
+int hbx_ctx_destroy(hbx_ctx* c) {
+  if (!c) return HBX_E_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  dbuf* bufs[] = {&c->pk,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
+                  &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
+                  &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
+                  &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own};
+  for (dbuf* b : bufs) b->release();
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return HBX_OK;
+}
+
+int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* status) {
+  if (!c || (!pk_comp && n)) return fail(c, HBX_E_INVALID_ARG, "hbx_set_pk_shares: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->pk.ensure((size_t)n * sizeof(g1a)) || !c->pk_status.ensure((size_t)n * 4) ||
+      !c->pk_comp.ensure((size_t)n * 48))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_pk_shares: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->pk_comp.p, pk_comp, (size_t)n * 48, hipMemcpyHostToDevice, c->stream));
+  if (n) {
+    hipLaunchKernelGGL(k_decompress_g1, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->pk_comp.as<uint8_t>(),
+                       n, c->pk.as<g1a>(), c->pk_status.as<int32_t>());
+    HIPCHK(c, hipGetLastError());
+  }
+  std::vector<int32_t> st(n);
+  HIPCHK(c, hipMemcpyAsync(st.data(), c->pk_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (status) memcpy(status, st.data(), (size_t)n * 4);
+  c->n_keys = n;
+  return HBX_OK;
+}
+
+int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
+                              const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
+                              uint64_t max_v_len, uint8_t* d_ct_valid, void* stream) {
+  if (!c || p == 0 || !d_u_comp || !d_v_off || !d_w_comp)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) ||
+      !c->lines.ensure((size_t)p * sizeof(line_block)) ||
+      !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
+      !c->ct_valid.ensure(p))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
+  const dim3 b64(64);
+  hipLaunchKernelGGL(k_prepare_ct, dim3((p + 63) / 64), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p,
+                     c->U.as<g1a>(), c->G2pts.as<g2a>(), c->ct_ok.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
+                     c->lines.as<line_pre>(), c->scratch.as<fq2>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_verify_ct, dim3((p + 63) / 64), b64, 0, s, c->U.as<g1a>(), c->G2pts.as<g2a>(),
+                     c->lines.as<line_block>(), p, c->ct_ok.as<uint8_t>(), c->ct_valid.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  if (d_ct_valid) HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, p, hipMemcpyDeviceToDevice, s));
+  c->p_ct = p;
+  c->d_v_blob = d_v_blob;
+  c->d_v_off = d_v_off;
+  c->max_v_len = max_v_len;
+  return HBX_OK;
+}
+
+int hbx_prepare_ciphertexts(hbx_ctx* c, const uint8_t* u_comp, const uint8_t* v_blob, const uint64_t* v_off,
+                            const uint8_t* w_comp, uint32_t p, uint8_t* ct_valid_bits) {
+  if (!c || p == 0 || !u_comp || !v_off || !w_comp)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t vbytes = v_off[p];
+  uint64_t maxv = 0;
+  for (uint32_t j = 0; j < p; j++) {
+    if (v_off[j + 1] < v_off[j]) return fail(c, HBX_E_INVALID_ARG, "v_off not monotone");
+    maxv = std::max<uint64_t>(maxv, v_off[j + 1] - v_off[j]);
+  }
+  if (!c->u_comp_own.ensure((size_t)p * 48) || !c->w_comp_own.ensure((size_t)p * 96) ||
+      !c->v_off_own.ensure((size_t)(p + 1) * 8) || !c->v_blob_own.ensure(vbytes ? vbytes : 16))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->u_comp_own.p, u_comp, (size_t)p * 48, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->w_comp_own.p, w_comp, (size_t)p * 96, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->v_off_own.p, v_off, (size_t)(p + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (vbytes) HIPCHK(c, hipMemcpyAsync(c->v_blob_own.p, v_blob, vbytes, hipMemcpyHostToDevice, c->stream));
+  int rc = hbx_prepare_ciphertexts_d(c, c->u_comp_own.as<uint8_t>(), c->v_blob_own.as<uint8_t>(),
+                                     c->v_off_own.as<uint64_t>(), c->w_comp_own.as<uint8_t>(), p, maxv,
+                                     nullptr, c->stream);
+  if (rc) return rc;
+  std::vector<uint8_t> ok(p);
+  HIPCHK(c, hipMemcpyAsync(ok.data(), c->ct_valid.p, p, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ct_valid_bits) pack_bits(ok.data(), p, ct_valid_bits);
+  return HBX_OK;
+}
+
+int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_present, uint32_t n,
+                            uint32_t p, uint8_t* d_valid, void* stream) {
+  if (!c || !d_shares || n == 0 || p == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_dec_shares_d: bad args");
+  if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
+  if (p != c->p_ct) return fail(c, HBX_E_NO_CIPHERTEXTS, "p=%u but %u ciphertexts prepared", p, c->p_ct);
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  const size_t m = (size_t)n * p;
+  if (!c->S.ensure(m * sizeof(g1a)) || !c->valid.ensure(m))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
+  hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, d_shares, d_present,
+                     c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines.as<line_block>(),
+                     c->ct_ok.as<uint8_t>(), n, c->S.as<g1a>(), c->valid.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  if (d_valid) HIPCHK(c, hipMemcpyAsync(d_valid, c->valid.p, m, hipMemcpyDeviceToDevice, s));
+  c->n_shares = n;
+  return HBX_OK;
+}
+
+int hbx_verify_dec_shares(hbx_ctx* c, const uint8_t* shares, const uint8_t* present_bits, uint32_t n,
+                          uint32_t p, uint8_t* valid_bits) {
+  if (!c || !shares || n == 0 || p == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_dec_shares: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t m = (size_t)n * p;
+  if (!c->shares_own.ensure(m * 48) || (present_bits && !c->present_own.ensure(m)))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->shares_own.p, shares, m * 48, hipMemcpyHostToDevice, c->stream));
+  std::vector<uint8_t> pres;
+  if (present_bits) {
+    pres.resize(m);
+    for (size_t k = 0; k < m; k++) pres[k] = (present_bits[k >> 3] >> (k & 7)) & 1;
+    HIPCHK(c, hipMemcpyAsync(c->present_own.p, pres.data(), m, hipMemcpyHostToDevice, c->stream));
+  }
+  int rc = hbx_verify_dec_shares_d(c, c->shares_own.as<uint8_t>(),
+                                   present_bits ? c->present_own.as<uint8_t>() : nullptr, n, p, nullptr,
+                                   c->stream);
+  if (rc) return rc;
+  std::vector<uint8_t> v(m);
+  HIPCHK(c, hipMemcpyAsync(v.data(), c->valid.p, m, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (valid_bits) pack_bits(v.data(), m, valid_bits);
+  return HBX_OK;
+}
+
+int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* d_status, void* stream) {
+  if (!c || t == 0 || t > (uint32_t)COMBINE_MAX_T || !d_out_blob)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt_d: bad args");
+  if (c->n_shares == 0 || c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  const uint32_t p = c->p_ct;
+  if (!c->keys.ensure((size_t)p * 32) || !c->status.ensure((size_t)p * 4))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_decrypt_d: out of device memory");
+  hipLaunchKernelGGL(k_combine, dim3(p), dim3(COMBINE_THREADS), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
+                     c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  const uint64_t blocks = (c->max_v_len + 15) / 16;
+  if (blocks) {
+    hipLaunchKernelGGL(k_keystream_xor, dim3((unsigned)((blocks + 63) / 64), p), dim3(64), 0, s,
+                       c->keys.as<uint32_t>(), c->status.as<int32_t>(), c->d_v_blob, c->d_v_off, d_out_blob);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (d_status) HIPCHK(c, hipMemcpyAsync(d_status, c->status.p, (size_t)p * 4, hipMemcpyDeviceToDevice, s));
+  return HBX_OK;
+}
+
+int hbx_combine_decrypt(hbx_ctx* c, uint32_t t, uint8_t* out_blob, int32_t* status) {
+  if (!c || !out_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no ciphertexts prepared");
+  std::vector<uint64_t> off(c->p_ct + 1);
+  HIPCHK(c, hipMemcpyAsync(off.data(), c->d_v_off, off.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t total = off[c->p_ct];
+  if (!c->out_own.ensure(total ? total : 16)) return fail(c, HBX_E_OUT_OF_MEMORY, "out of device memory");
+  HIPCHK(c, hipMemsetAsync(c->out_own.p, 0, total ? total : 16, c->stream));
+  int rc = hbx_combine_decrypt_d(c, t, c->out_own.as<uint8_t>(), nullptr, c->stream);
+  if (rc) return rc;
+  if (total) HIPCHK(c, hipMemcpyAsync(out_blob, c->out_own.p, total, hipMemcpyDeviceToHost, c->stream));
+  std::vector<int32_t> st(c->p_ct);
+  HIPCHK(c, hipMemcpyAsync(st.data(), c->status.p, (size_t)c->p_ct * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (status) memcpy(status, st.data(), st.size() * 4);
+  return HBX_OK;
+}
+
+}  // extern "C"

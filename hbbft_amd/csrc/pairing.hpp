@@ -1,0 +1,168 @@
+// Optimal-ate pairing pieces for the batched BLS12-381 checks (pairing 0.14.2 `Bls12::pairing`
+// = miller_loop + final_exponentiation, reached from threshold_crypto at honey_badger.rs:229,
+// :371 and common_coin.rs:151, :196).
+//
+// MI355X-first restructuring (result bits identical to two independent pairings):
+//  * every check e(A, Q1) == e(B, Q2) is evaluated as e(A, Q1) * e(-B, Q2) == 1 with ONE shared
+//    Miller loop over both pairs and ONE final exponentiation;
+//  * G2 arguments that are per-proposer constants (H_j = hash_g1_g2(U_j, V_j) and W_j) are
+//    "prepared" once: the 68 line functions of the loop are stored normalised so that the y_P
+//    coefficient is 1, as two Fq2 coefficients (c0, c1):  l(P) = c0 + (c1 x_P) v + y_P v w.
+//    All lanes of a workgroup read the same coefficients (wave-uniform loads).
+//  * the hard part of the final exponentiation uses 3 Phi_12(p)/r = (x-1)^2 (x+p)(x^2+p^2-1) + 3
+//    (computes e^3; e^3 == 1 <=> e == 1 since gcd(3, r) = 1) with Granger-Scott cyclotomic
+//    squarings.
+#pragma once
+#include "curve.hpp"
+
+namespace hbx {
+
+// |x| = 0xd201000000010000: 63 doubling steps after the leading bit, 5 addition steps.
+constexpr int MILLER_LINES = 68;
+
+struct line_pre {
+  fq2 c0, c1;
+};
+
+// Raw line through the doubling of T (Jacobian), scaled by 2 Y Z^3:
+//   c0 = 3X^3 - 2Y^2, c1 = -3X^2 Z^2, c2 = 2YZ^3;  T <- 2T.
+HBX_HDNI void line_dbl_step(g2j& T, fq2& c0, fq2& c1, fq2& c2) {
+  const fq2 A = fq2_sqr(T.x);
+  const fq2 B = fq2_sqr(T.y);
+  const fq2 C = fq2_sqr(B);
+  const fq2 ZZ = fq2_sqr(T.z);
+  const fq2 E = fq2_add(fq2_dbl(A), A);
+  c0 = fq2_sub(fq2_mul(E, T.x), fq2_dbl(B));
+  c1 = fq2_neg(fq2_mul(E, ZZ));
+  fq2 D = fq2_sub(fq2_sub(fq2_sqr(fq2_add(T.x, B)), A), C);
+  D = fq2_dbl(D);
+  const fq2 F = fq2_sqr(E);
+  const fq2 X3 = fq2_sub(F, fq2_dbl(D));
+  const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
+  const fq2 Y3 = fq2_sub(fq2_mul(E, fq2_sub(D, X3)), C8);
+  const fq2 Z3 = fq2_dbl(fq2_mul(T.y, T.z));
+  c2 = fq2_mul(Z3, ZZ);
+  T = g2j{X3, Y3, Z3};
+}
+
+// Raw line through T and the affine base point Q, slope lambda = num/den with
+// num = Y - yQ Z^3, den = Z (X - xQ Z^2); scaled by den:
+//   c0 = num xQ - yQ den, c1 = -num, c2 = den;  T <- T + Q.
+HBX_HDNI void line_add_step(g2j& T, const g2a& Q, fq2& c0, fq2& c1, fq2& c2) {
+  const fq2 Z1Z1 = fq2_sqr(T.z);
+  const fq2 U2 = fq2_mul(Q.x, Z1Z1);
+  const fq2 S2 = fq2_mul(fq2_mul(Q.y, T.z), Z1Z1);
+  const fq2 H = fq2_sub(U2, T.x);           // = -(X - xQ Z^2)
+  const fq2 num = fq2_sub(T.y, S2);         // Y - yQ Z^3
+  const fq2 den = fq2_neg(fq2_mul(T.z, H)); // Z (X - xQ Z^2)
+  c0 = fq2_sub(fq2_mul(num, Q.x), fq2_mul(Q.y, den));
+  c1 = fq2_neg(num);
+  c2 = den;
+  // madd-2007-bl
+  const fq2 HH = fq2_sqr(H);
+  const fq2 I = fq2_dbl(fq2_dbl(HH));
+  const fq2 J = fq2_mul(H, I);
+  const fq2 r = fq2_dbl(fq2_sub(S2, T.y));
+  const fq2 V = fq2_mul(T.x, I);
+  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr(r), J), fq2_dbl(V));
+  const fq2 Y3 = fq2_sub(fq2_mul(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul(T.y, J)));
+  const fq2 Z3 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(T.z, H)), Z1Z1), HH);
+  T = g2j{X3, Y3, Z3};
+}
+
+// Prepare the 68 normalised lines of Q (affine, not infinity).  `scratch` holds 2*68 Fq2 of
+// per-lane workspace (raw c2 values and their prefix products for one batched inversion).
+HBX_HDNI void g2_prepare_lines(const g2a& Q, line_pre* out, fq2* scratch) {
+  g2j T = g2_from_affine(Q);
+  fq2 pp = fq2_one();
+  int k = 0;
+  for (int i = 62; i >= 0; i--) {
+    fq2 c0, c1, c2;
+    line_dbl_step(T, c0, c1, c2);
+    out[k].c0 = c0;
+    out[k].c1 = c1;
+    pp = fq2_mul(pp, c2);
+    scratch[2 * k] = c2;
+    scratch[2 * k + 1] = pp;
+    k++;
+    if ((BLS_X >> i) & 1) {
+      line_add_step(T, Q, c0, c1, c2);
+      out[k].c0 = c0;
+      out[k].c1 = c1;
+      pp = fq2_mul(pp, c2);
+      scratch[2 * k] = c2;
+      scratch[2 * k + 1] = pp;
+      k++;
+    }
+  }
+  fq2 inv = fq2_inv(pp);
+  for (int j = MILLER_LINES - 1; j >= 0; j--) {
+    const fq2 prev = j > 0 ? scratch[2 * (j - 1) + 1] : fq2_one();
+    const fq2 c2inv = fq2_mul(inv, prev);
+    inv = fq2_mul(inv, scratch[2 * j]);
+    out[j].c0 = fq2_mul(out[j].c0, c2inv);
+    out[j].c1 = fq2_mul(out[j].c1, c2inv);
+  }
+}
+
+// f *= l(P) for a prepared line: l(P) = c0 + (c1 x_P) v + y_P v w.
+HBX_HDNI fq12 mul_by_line(const fq12& f, const line_pre& l, const g1a& P) {
+  const fq2 c1 = fq2_mul_fq(l.c1, P.x);
+  return fq12_mul_by_014(f, l.c0, c1, P.y);
+}
+
+// Product of two Miller loops f_{|x|,QA}(PA) * f_{|x|,QB}(PB) over prepared lines, conjugated
+// for x < 0.  PA / PB are affine; a pair whose `use` flag is false contributes 1 (a pairing
+// with the identity).
+HBX_HDNI fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const line_pre* LB,
+                           const g1a& PB, bool useB) {
+  fq12 f = fq12_one();
+  int k = 0;
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12_sqr(f);
+    if (useA) f = mul_by_line(f, LA[k], PA);
+    if (useB) f = mul_by_line(f, LB[k], PB);
+    k++;
+    if ((BLS_X >> i) & 1) {
+      if (useA) f = mul_by_line(f, LA[k], PA);
+      if (useB) f = mul_by_line(f, LB[k], PB);
+      k++;
+    }
+  }
+  return fq12_conj(f);
+}
+
+// g^|x| for g in the cyclotomic subgroup.
+HBX_HDNI fq12 cyc_exp_abs_x(const fq12& g) {
+  fq12 r = g;
+  for (int i = 62; i >= 0; i--) {
+    r = fq12_cyclotomic_sqr(r);
+    if ((BLS_X >> i) & 1) r = fq12_mul(r, g);
+  }
+  return r;
+}
+// g^x (x negative) = conj(g^|x|) in the cyclotomic subgroup.
+HBX_HD fq12 cyc_exp_x(const fq12& g) { return fq12_conj(cyc_exp_abs_x(g)); }
+
+// f^(3 (p^12 - 1)/r)
+HBX_HDNI fq12 final_exponentiation(const fq12& f) {
+  // easy part: f^((p^6 - 1)(p^2 + 1))
+  fq12 t = fq12_mul(fq12_conj(f), fq12_inv(f));
+  t = fq12_mul(fq12_frobenius2(t), t);
+  // hard part
+  fq12 a = fq12_mul(cyc_exp_x(t), fq12_conj(t));      // t^(x-1)
+  a = fq12_mul(cyc_exp_x(a), fq12_conj(a));            // t^((x-1)^2)
+  fq12 b = fq12_mul(cyc_exp_x(a), fq12_frobenius(a));  // a^(x+p)
+  fq12 c = fq12_mul(cyc_exp_x(cyc_exp_x(b)), fq12_frobenius2(b));
+  c = fq12_mul(c, fq12_conj(b));                        // b^(x^2 + p^2 - 1)
+  const fq12 t3 = fq12_mul(fq12_cyclotomic_sqr(t), t);  // t^3
+  return fq12_mul(c, t3);
+}
+
+// e(PA, QA) * e(PB, QB) == 1 with prepared lines for QA, QB.
+HBX_HD bool pairing_check2(const line_pre* LA, const g1a& PA, const line_pre* LB, const g1a& PB) {
+  const fq12 f = miller_loop2(LA, PA, true, LB, PB, true);
+  return fq12_is_one(final_exponentiation(f));
+}
+
+}  // namespace hbx

@@ -1,0 +1,184 @@
+"""ctypes binding of the C ABI in ``include/hbx.h`` (``hbbft_amd/libhbx.so``).
+
+This is plumbing for tests, the bench and Python callers; the product is the C ABI itself.
+There is deliberately no CPU fallback: if ``libhbx.so`` is missing or no HIP device is present,
+construction fails with an exception naming what is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhbx.so")
+
+HBX_OK = 0
+HBX_E_INVALID_ARG = -1
+HBX_E_DEVICE = -2
+HBX_E_NOT_ENOUGH_SHARES = -3
+HBX_E_DUPLICATE_ENTRY = -4
+HBX_E_NO_KEYS = -5
+HBX_E_NO_CIPHERTEXTS = -6
+HBX_E_INVALID_CIPHERTEXT = -7
+HBX_E_OUT_OF_MEMORY = -8
+
+# Every symbol include/hbx.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "hbx_ctx_create",
+    "hbx_ctx_destroy",
+    "hbx_last_error",
+    "hbx_version",
+    "hbx_set_pk_shares",
+    "hbx_prepare_ciphertexts",
+    "hbx_verify_dec_shares",
+    "hbx_combine_decrypt",
+    "hbx_prepare_ciphertexts_d",
+    "hbx_verify_dec_shares_d",
+    "hbx_combine_decrypt_d",
+)
+
+_lib = None
+
+
+class HbxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hbx error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libhbx.so (raises OSError with the path if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    u32 = ctypes.c_uint32
+    lib.hbx_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+    lib.hbx_ctx_destroy.argtypes = [P]
+    lib.hbx_last_error.argtypes = [P]
+    lib.hbx_last_error.restype = ctypes.c_char_p
+    lib.hbx_version.restype = ctypes.c_char_p
+    lib.hbx_set_pk_shares.argtypes = [P, u8p, u32, i32p]
+    lib.hbx_prepare_ciphertexts.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
+    lib.hbx_verify_dec_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
+    lib.hbx_combine_decrypt.argtypes = [P, u32, u8p, i32p]
+    lib.hbx_prepare_ciphertexts_d.argtypes = [P, P, P, P, P, u32, ctypes.c_uint64, P, P]
+    lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
+    lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
+    _lib = lib
+    return lib
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def pack_bits(bools) -> np.ndarray:
+    a = np.asarray(bools, dtype=np.uint8).reshape(-1)
+    return np.packbits(a, bitorder="little")
+
+
+def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:
+    return np.unpackbits(np.asarray(bits, dtype=np.uint8), bitorder="little")[:n].astype(bool)
+
+
+class Context:
+    """One hbx context bound to a HIP device (``hbx_ctx_create``)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.hbx_ctx_create(device, ctypes.byref(h))
+        if rc != HBX_OK:
+            raise HbxError(rc, f"hbx_ctx_create(device={device}) failed: no usable HIP device?")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.hbx_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != HBX_OK:
+            raise HbxError(rc, self.lib.hbx_last_error(self.h).decode())
+
+    # -- host API ------------------------------------------------------------------------------
+    def set_pk_shares(self, pk_comp: Sequence[bytes]) -> np.ndarray:
+        n = len(pk_comp)
+        buf = np.frombuffer(b"".join(pk_comp), dtype=np.uint8).copy()
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self.lib.hbx_set_pk_shares(self.h, _u8(buf), n, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return st
+
+    def prepare_ciphertexts(self, cts) -> np.ndarray:
+        """cts: list of (u_comp48, v_bytes, w_comp96).  Returns bool[p] = Ciphertext::verify."""
+        p = len(cts)
+        u = np.frombuffer(b"".join(c[0] for c in cts), dtype=np.uint8).copy()
+        w = np.frombuffer(b"".join(c[2] for c in cts), dtype=np.uint8).copy()
+        off = np.zeros(p + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(c[1]) for c in cts])
+        vb = np.frombuffer(b"".join(c[1] for c in cts) or b"\0", dtype=np.uint8).copy()
+        bits = np.zeros((p + 7) // 8, dtype=np.uint8)
+        self._check(self.lib.hbx_prepare_ciphertexts(
+            self.h, _u8(u), _u8(vb), off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _u8(w), p, _u8(bits)))
+        self._v_off = off
+        return unpack_bits(bits, p)
+
+    def verify_dec_shares(self, shares: np.ndarray, present: Optional[np.ndarray] = None) -> np.ndarray:
+        """shares: uint8[p, n, 48].  Returns bool[p, n]."""
+        shares = np.ascontiguousarray(shares, dtype=np.uint8)
+        p, n, _ = shares.shape
+        pres = None if present is None else pack_bits(np.asarray(present, dtype=bool).reshape(-1))
+        bits = np.zeros((p * n + 7) // 8, dtype=np.uint8)
+        self._check(self.lib.hbx_verify_dec_shares(
+            self.h, _u8(shares), None if pres is None else _u8(pres), n, p, _u8(bits)))
+        return unpack_bits(bits, p * n).reshape(p, n)
+
+    def combine_decrypt(self, t: int):
+        """Returns (list of plaintext bytes or None, status int32[p])."""
+        off = self._v_off
+        p = len(off) - 1
+        out = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
+        st = np.zeros(p, dtype=np.int32)
+        self._check(self.lib.hbx_combine_decrypt(self.h, t, _u8(out), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        res = []
+        for j in range(p):
+            res.append(out[int(off[j]):int(off[j + 1])].tobytes() if st[j] == HBX_OK else None)
+        return res, st
+
+    # -- device API (torch tensors as HBM buffers; torch is plumbing only) -----------------------
+    def prepare_ciphertexts_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_ct_valid=None, stream=None):
+        self._check(self.lib.hbx_prepare_ciphertexts_d(
+            self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
+            None if d_ct_valid is None else d_ct_valid.data_ptr(), stream))
+
+    def verify_dec_shares_d(self, d_shares, n: int, p: int, d_valid=None, d_present=None, stream=None):
+        self._check(self.lib.hbx_verify_dec_shares_d(
+            self.h, d_shares.data_ptr(), None if d_present is None else d_present.data_ptr(), n, p,
+            None if d_valid is None else d_valid.data_ptr(), stream))
+
+    def combine_decrypt_d(self, t: int, d_out, d_status=None, stream=None):
+        self._check(self.lib.hbx_combine_decrypt_d(
+            self.h, t, d_out.data_ptr(), None if d_status is None else d_status.data_ptr(), stream))

@@ -1,0 +1,122 @@
+/* hbx.h -- C ABI of the MI355X batch engine for hbbft's threshold-crypto hot path.
+ *
+ * Drop-in boundary.  The reference calls threshold_crypto / pairing 0.14 one
+ * share at a time on the caller's thread; this ABI takes a whole epoch's worth in one call.  Each
+ * entry point names the reference interface it replaces (file:line in jonnydubowsky/hbbft @ v0).
+ *
+ * Conventions
+ *  - Plain pointers + sizes, caller-owned buffers, no torch types.
+ *  - Functions without the `_d` suffix take HOST pointers, stage through device buffers owned
+ *    by the context and block until results are back on the host.
+ *  - Functions with the `_d` suffix take DEVICE pointers (hipMalloc'd on the context's device)
+ *    and a hipStream_t passed as `void*` (NULL = the context's own stream); they enqueue work
+ *    and return without synchronising.
+ *  - Return value: HBX_OK (0) or a negative HBX_E_* code.  A failed verification is NOT an error:
+ *    it is a 0 in the corresponding validity output, exactly as the reference returns `false`.
+ *  - Validity outputs are byte-per-item (1 = valid) in the `_d` API and little-endian bitmaps
+ *    (bit k of byte k/8) in the host API.
+ *  - Point encodings are the zcash/pairing 0.14 formats: G1 compressed 48 B, G2 compressed
+ *    96 B, G2 uncompressed 192 B (x.c1 || x.c0 || y.c1 || y.c0).
+ *  - Share matrices are proposer-major: share[j][i] = the decryption share node i sent for
+ *    proposer j's ciphertext, at offset (j * n + i) * 48.
+ *  - One context per device.  Calls on one context must be serialised by the caller.
+ */
+#ifndef HBX_H
+#define HBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBX_OK 0
+#define HBX_E_INVALID_ARG (-1)
+#define HBX_E_DEVICE (-2)
+#define HBX_E_NOT_ENOUGH_SHARES (-3) /* threshold_crypto Error::NotEnoughShares */
+#define HBX_E_DUPLICATE_ENTRY (-4)   /* threshold_crypto Error::DuplicateEntry */
+#define HBX_E_NO_KEYS (-5)           /* hbx_set_pk_shares not called / wrong n */
+#define HBX_E_NO_CIPHERTEXTS (-6)    /* hbx_prepare_ciphertexts not called / wrong p */
+#define HBX_E_INVALID_CIPHERTEXT (-7)/* Ciphertext::verify failed or undecodable (honey_badger.rs:366-373) */
+#define HBX_E_OUT_OF_MEMORY (-8)
+
+/* per-point decode status (hbx_set_pk_shares / hbx_prepare_ciphertexts) */
+#define HBX_PT_OK 0
+#define HBX_PT_BAD_FLAGS 1
+#define HBX_PT_NOT_IN_FIELD 2
+#define HBX_PT_NOT_ON_CURVE 3
+#define HBX_PT_INFINITY 4
+
+typedef struct hbx_ctx hbx_ctx;
+
+/* Create / destroy a context bound to HIP device `device`. */
+int hbx_ctx_create(int device, hbx_ctx** out);
+int hbx_ctx_destroy(hbx_ctx* ctx);
+/* Human-readable description of the last error on this context (never NULL). */
+const char* hbx_last_error(const hbx_ctx* ctx);
+/* Library version string, e.g. "hbx 0.1.0 gfx950". */
+const char* hbx_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Key material (once per era).
+ * Replaces: NetworkInfo::new's public_key_share derivation (src/messaging.rs:251-254) and the
+ * per-call lookup NetworkInfo::public_key_share (src/messaging.rs:312) used by
+ * HoneyBadger::verify_decryption_share (src/honey_badger/honey_badger.rs:228-232).
+ * pk_comp: n x 48 B compressed pk_i (node index order = BTreeMap order, messaging.rs:246-250).
+ * status (optional, n entries): HBX_PT_* per key.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_set_pk_shares(hbx_ctx* ctx, const uint8_t* pk_comp, uint32_t n, int32_t* status);
+
+/* ---------------------------------------------------------------------------------------------
+ * Ciphertexts of one epoch (one per accepted proposer).
+ * Replaces: threshold_crypto Ciphertext::verify (src/honey_badger/honey_badger.rs:371) and
+ * hoists hash_g1_g2(U_j, V_j) -- recomputed by the reference inside every
+ * verify_decryption_share call -- to once per ciphertext.
+ * u_comp: p x 48 B; w_comp: p x 96 B; v_blob + v_off[p + 1]: the V byte strings.
+ * ct_valid_bits: ceil(p/8) B out; bit j = Ciphertext::verify(ct_j) (0 also for undecodable
+ * points, i.e. the reference's InvalidCiphertext / ShareDecryptionFailed faults).
+ * ------------------------------------------------------------------------------------------- */
+int hbx_prepare_ciphertexts(hbx_ctx* ctx, const uint8_t* u_comp, const uint8_t* v_blob,
+                            const uint64_t* v_off, const uint8_t* w_comp, uint32_t p,
+                            uint8_t* ct_valid_bits);
+
+/* ---------------------------------------------------------------------------------------------
+ * Decryption-share verification, whole epoch.
+ * Replaces: PublicKeyShare::verify_decryption_share (src/honey_badger/honey_badger.rs:229) as
+ * called from verify_pending_decryption_shares (:422-444) and handle_decryption_share_message
+ * (:198).  valid[j][i] = e(S_ji, H_j) == e(pk_i, W_j).  Absent shares (present bit 0), unknown
+ * senders (i >= n of hbx_set_pk_shares) and undecodable encodings give 0.
+ * shares: p x n x 48 B; present_bits: ceil(p*n/8) B (NULL = all present);
+ * valid_bits: ceil(p*n/8) B out (bit j*n + i).
+ * ------------------------------------------------------------------------------------------- */
+int hbx_verify_dec_shares(hbx_ctx* ctx, const uint8_t* shares, const uint8_t* present_bits,
+                          uint32_t n, uint32_t p, uint8_t* valid_bits);
+
+/* ---------------------------------------------------------------------------------------------
+ * Threshold decryption of every proposer's contribution.
+ * Replaces: PublicKeySet::decrypt (src/honey_badger/honey_badger.rs:340) inside
+ * try_decrypt_proposer_contribution (:315-349): for each proposer j takes the FIRST t valid
+ * shares in node-index order, Lagrange-interpolates at 0 (x = index + 1) and XORs V_j with
+ * hash_bytes(g, |V_j|).  Uses the shares and validity of the last hbx_verify_dec_shares call.
+ * out_blob: sum |V_j| bytes at the v_off offsets of hbx_prepare_ciphertexts.
+ * status: p entries, HBX_OK / HBX_E_NOT_ENOUGH_SHARES / HBX_E_INVALID_CIPHERTEXT.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_combine_decrypt(hbx_ctx* ctx, uint32_t t, uint8_t* out_blob, int32_t* status);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device-pointer / stream variants (inputs resident in HBM; nothing is copied to the host).
+ *   d_valid / d_ct_valid / d_present are byte-per-item arrays.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_prepare_ciphertexts_d(hbx_ctx* ctx, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
+                              const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
+                              uint64_t max_v_len, uint8_t* d_ct_valid, void* stream);
+int hbx_verify_dec_shares_d(hbx_ctx* ctx, const uint8_t* d_shares, const uint8_t* d_present,
+                            uint32_t n, uint32_t p, uint8_t* d_valid, void* stream);
+int hbx_combine_decrypt_d(hbx_ctx* ctx, uint32_t t, uint8_t* d_out_blob, int32_t* d_status,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBX_H */

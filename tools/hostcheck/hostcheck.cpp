@@ -1,0 +1,56 @@
+// Developer tool: builds the HIP kernels' __host__ __device__ arithmetic for the CPU so it can be
+// unit-tested against the Python oracle in a container without a GPU.  NOT part of the product
+// (libhbx.so never contains or calls this); see tests/test_hostcheck.py.
+#include <cstring>
+#include "../../hbbft_amd/csrc/pairing.hpp"
+#include "../../hbbft_amd/csrc/hash.hpp"
+using namespace hbx;
+extern "C" {
+// canonical big-endian 48-byte operands
+void hc_fq_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  fq x = fq_to_mont(fq_from_be(a)), y = fq_to_mont(fq_from_be(b));
+  fq_to_be(fq_from_mont(fq_mul(x, y)), out);
+}
+void hc_fq_inv(const uint8_t* a, uint8_t* out) {
+  fq x = fq_to_mont(fq_from_be(a));
+  fq_to_be(fq_from_mont(fq_inv(x)), out);
+}
+int hc_g1_roundtrip(const uint8_t* in48, uint8_t* out48) {
+  g1a p; int st = g1_decompress(in48, p);
+  if (st != HBX_PT_OK && st != HBX_PT_INFINITY) return st;
+  g1_compress(p, out48); return st;
+}
+int hc_g2_roundtrip(const uint8_t* in96, uint8_t* out96) {
+  g2a p; int st = g2_decompress(in96, p);
+  if (st != HBX_PT_OK && st != HBX_PT_INFINITY) return st;
+  g2_compress(p, out96); return st;
+}
+// returns 1 if e(PA,QA) e(PB,QB) == 1, 0 if not, negative on decode failure
+int hc_pairing_check2(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK) return -1;
+  if (g1_decompress(pb, PB) != HBX_PT_OK) return -2;
+  if (g2_decompress(qa, QA) != HBX_PT_OK) return -3;
+  if (g2_decompress(qb, QB) != HBX_PT_OK) return -4;
+  static line_pre LA[MILLER_LINES], LB[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  g2_prepare_lines(QB, LB, scratch);
+  return pairing_check2(LA, PA, LB, PB) ? 1 : 0;
+}
+int hc_g2_mul_cofactor(const uint8_t* in96, uint8_t* out96) {
+  g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
+  g2j r = g2_mul_bits(g2_from_affine(p), G2_COFACTOR, G2_COFACTOR_BITS);
+  g2_compress(g2_to_affine(r), out96); return 0;
+}
+}
+extern "C" {
+void hc_sha256(const uint8_t* m, uint64_t n, uint8_t* out32) { sha256_2(m, n, nullptr, 0, out32); }
+int hc_hash_g1_g2(const uint8_t* u48, const uint8_t* v, uint64_t vlen, uint8_t* out96) {
+  g2j h = hash_g1_g2(u48, v, vlen);
+  g2_compress(g2_to_affine(h), out96); return 0;
+}
+int hc_hash_g2_digest(const uint8_t* d32, uint8_t* out96) {
+  g2_compress(g2_to_affine(hash_g2_from_digest(d32)), out96); return 0;
+}
+}
