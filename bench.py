@@ -1,0 +1,263 @@
+"""Benchmark: one HoneyBadger node-epoch of threshold-decryption crypto at N=256 on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--vlen 1024] [--no-cpu-baseline]
+
+A *step* is the crypto of one HoneyBadger epoch as one node sees it (SURVEY.md §3 stack A,
+BASELINE.json configs[2]): for every one of the N accepted proposals
+  * ``Ciphertext::verify`` + the hoisted ``hash_g1_g2(U_j, V_j)``  (honey_badger.rs:371),
+  * ``verify_decryption_share`` for all N senders                  (honey_badger.rs:229, :422-444),
+  * ``PublicKeySet::decrypt`` with the first f+1 valid shares      (honey_badger.rs:340),
+i.e. 65,536 share verifications + 256 ciphertext checks + 256 Lagrange combines (t = 86) + the
+hash_bytes keystream XOR, through the C ABI of libhbx.so on device-resident inputs.
+
+Multi-GPU (``torchrun``): the epoch is sharded by proposer column (rank g owns proposers
+[g P/G, (g+1) P/G) with their ciphertexts and share columns; keys are replicated); after the
+combine one RCCL all-gather assembles the validity bytes, ciphertext bits and per-proposer status.
+Total work is fixed as G grows -> "scaling": "strong".
+
+Inputs (synthetic, seeded): keys from ``hbbft_amd.netinfo.generate_keys``; 1 KiB random
+contributions; U/V/W made by ``hbx_encrypt`` and shares by ``hbx_decrypt_shares`` on the GPU; 1 in
+64 shares replaced by the same sender's share of a DIFFERENT ciphertext (the reference's
+FaultyShareAdversary, tests/honey_badger.rs:99-106).  After the timed steps the validity matrix
+must equal "not corrupted" and every plaintext must equal its contribution, or the bench fails.
+
+Roofline: the dominant kernel is the share verification (k_verify_shares).  Its algorithmic work
+is 16,027 Fq multiplications per share (tools/opcount: decompress 486 + 2-pair Miller loop 7,400
++ final exponentiation 8,141) x 288 32-bit multiply-adds each; its launch time is measured with
+HIP events recorded on the stream it runs on.  The bound is integer VALU (v_mad_u64_u32), not HBM
+or MFMA; the peak is the measured chip rate from tools/microbench.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# Algorithmic work per unit (tools/opcount/opcount.cpp)
+FQMUL_PER_SHARE_VERIFY = 16027
+MADS_PER_FQMUL = 288
+# Chip peak of 32x32->64-bit integer multiply-add (v_mad_u64_u32), measured by
+# tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.
+PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=256, help="validators N (shares per ciphertext)")
+    ap.add_argument("--vlen", type=int, default=1024, help="contribution bytes per proposer")
+    ap.add_argument("--corrupt-every", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
+    """Synthetic inputs of proposers [lo, hi) of one epoch, built on the GPU (hbx producer API)."""
+    from hbbft_amd import netinfo
+
+    sks, sk_shares, master_sk = netinfo.generate_keys(n)
+    pk_shares = ctx.public_keys(sk_shares)
+    master_pk = ctx.public_keys(master_sk)[0].tobytes()
+    rng = np.random.default_rng(0x68626278_00000002)
+    msgs_all = [rng.integers(0, 256, size=vlen, dtype=np.uint8).tobytes() for _ in range(n)]
+    r_all = netinfo.scalars_to_be32(netinfo.random_scalars(np.random.default_rng(0x68626278_00000003), n + 1))
+    pj = hi - lo
+    # own proposers plus one foreign ciphertext (index n) whose shares serve as corruptions
+    idx = list(range(lo, hi)) + [n]
+    foreign_msg = b"foreign ciphertext"
+    msgs = [msgs_all[j] for j in range(lo, hi)] + [foreign_msg]
+    cts = ctx.encrypt(master_pk, msgs, r_all[idx])
+    u48 = np.stack([np.frombuffer(c[0], dtype=np.uint8) for c in cts])
+    shares = ctx.decrypt_shares(sk_shares, u48)  # (pj + 1, n, 48)
+    crng = np.random.default_rng(0x68626278_00000004)
+    corrupt = crng.integers(0, corrupt_every, size=(n, n)) == 0  # global (proposer, sender) pattern
+    corrupt = corrupt[lo:hi]
+    sh = shares[:pj].copy()
+    ii = np.nonzero(corrupt)
+    sh[ii[0], ii[1]] = shares[pj, ii[1]]
+    return dict(pk_shares=pk_shares, cts=cts[:pj], msgs=msgs[:pj], shares=sh, corrupt=corrupt, t=sks.threshold + 1)
+
+
+def cpu_baseline(ep, seconds: float):
+    """Oracle ("port") timing: the reference's per-share algorithm shape -- hash_g1_g2 recomputed
+    per share plus two full pairings (threshold_crypto verify_decryption_share as called at
+    honey_badger.rs:229) -- on a bounded sample of this workload's shares, one core."""
+    from oracle import bls12_381 as bls
+    from oracle import threshold as tc
+
+    pks = [bls.g1_decompress(bytes(b)) for b in ep["pk_shares"]]
+    done = 0
+    ok = 0
+    t0 = time.perf_counter()
+    j = 0
+    while True:
+        u, v, w = ep["cts"][j % len(ep["cts"])]
+        ct = (bls.g1_decompress(u), v, bls.g2_decompress(w))
+        i = (7 * done) % len(pks)
+        s = bls.g1_decompress(bytes(ep["shares"][j % len(ep["cts"]), i]))
+        ok += tc.verify_decryption_share(pks[i], s, ct) == (not ep["corrupt"][j % len(ep["cts"]), i])
+        done += 1
+        j += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    assert ok == done, "oracle disagrees with the expected validity on the CPU sample"
+    return dict(value=done / dt, unit="share verifies/s", cores=1, kind="port",
+                sample=f"{done} share verifications of the N={len(pks)} epoch (per-share hash_g1_g2 + 2 pairings, "
+                       f"pure-Python oracle, {dt:.1f} s)")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from hbbft_amd import shard
+    from hbbft_amd.hbx import Context
+
+    n = args.n
+    lo, hi = shard.proposer_range(n, world, rank)
+    pj = hi - lo
+    ctx = Context(local)
+    ep = make_epoch(ctx, n, lo, hi, args.vlen, args.corrupt_every)
+    st = ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]])
+    assert (st == 0).all()
+
+    # a dedicated stream: torch's default stream is the NULL handle, which the C ABI maps to the
+    # context's own stream -- HIP events must be recorded on the stream the kernels run on
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sh = stream.cuda_stream
+    assert sh != 0
+    cts = ep["cts"]
+    d_u = torch.from_numpy(np.stack([np.frombuffer(c[0], dtype=np.uint8) for c in cts])).to(dev)
+    d_w = torch.from_numpy(np.stack([np.frombuffer(c[2], dtype=np.uint8) for c in cts])).to(dev)
+    off = np.zeros(pj + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(c[1]) for c in cts])
+    d_off = torch.from_numpy(off).to(dev)
+    d_v = torch.from_numpy(np.frombuffer(b"".join(c[1] for c in cts), dtype=np.uint8).copy()).to(dev)
+    d_shares = torch.from_numpy(ep["shares"]).to(dev)
+    d_out = torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev)
+    # result slab gathered across ranks: [valid pj*n | ct_valid pj | status pj*4]
+    lay = shard.slab_layout(n, pj)
+    slab = torch.zeros(lay["size"], dtype=torch.uint8, device=dev)
+    d_valid = slab[lay["valid"][0]:lay["valid"][1]]
+    d_ct_valid = slab[lay["ct_valid"][0]:lay["ct_valid"][1]]
+    d_status = slab[lay["status"][0]:lay["status"][1]].view(torch.int32)
+    gathered = [None]
+    t = ep["t"]
+    maxv = int(np.max(np.diff(off)))
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+
+    def step(events=None):
+        if events:
+            events[0].record(stream)
+        ctx.prepare_ciphertexts_d(d_u, d_v, d_off, d_w, pj, maxv, d_ct_valid=d_ct_valid, stream=sh)
+        if events:
+            events[1].record(stream)
+        ctx.verify_dec_shares_d(d_shares, n, pj, d_valid=d_valid, stream=sh)
+        if events:
+            events[2].record(stream)
+        ctx.combine_decrypt_d(t, d_out, d_status=d_status, stream=sh)
+        if events:
+            events[3].record(stream)
+        if world > 1:
+            gathered[0] = shard.all_gather_slabs(slab, world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # correctness of the last step (size-independent properties)
+    valid = d_valid.cpu().numpy().reshape(pj, n).astype(bool)
+    expect = ~ep["corrupt"]
+    assert (d_ct_valid.cpu().numpy() == 1).all(), "a valid ciphertext failed Ciphertext::verify"
+    assert (valid == expect).all(), f"validity mismatch at {int((valid != expect).sum())} positions"
+    assert (d_status.cpu().numpy() == 0).all(), "combine status"
+    out = d_out.cpu().numpy()
+    for j in range(pj):
+        assert out[off[j]:off[j + 1]].tobytes() == ep["msgs"][j], f"plaintext {lo + j} differs"
+    if world > 1:
+        gv, gct, gst = shard.assemble(gathered[0].cpu().numpy(), n, world)
+        full = np.random.default_rng(0x68626278_00000004).integers(0, args.corrupt_every, size=(n, n)) == 0
+        assert (gv == ~full).all() and gct.all() and (gst == 0).all(), "gathered epoch result"
+
+    ms_prep = np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)])
+    ms_ver = np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)])
+    ms_comb = np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(args.steps)])
+    ms_step = elapsed / args.steps * 1e3
+    verifies = n * n
+    value = verifies * args.steps / elapsed
+    shares_here = pj * n
+    achieved = shares_here * FQMUL_PER_SHARE_VERIFY * MADS_PER_FQMUL / (ms_ver * 1e-3) / 1e12
+    res = {
+        "metric": "BLS12-381 share verifies/sec (node) at N=256; crypto ms per HB epoch",
+        "value": round(value, 1),
+        "unit": "share verifies/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32 (Fq 12x32-bit Montgomery limbs)",
+        "data": "synthetic (seeded keys, 1 KiB random contributions, GPU-made ciphertexts/shares, 1/64 foreign-ciphertext shares)",
+        "config": {"workload": f"HoneyBadger epoch N={n}: {verifies} decryption-share verifies + {n} Ciphertext::verify + "
+                               f"{n} combines (t={t}) + decrypt, |v|={args.vlen} B",
+                   "n": n, "t": t, "proposers_per_gpu": pj, "parallelism": f"proposer-column x{world}"},
+        "phases_ms": {"prepare_ciphertexts": round(float(ms_prep), 3), "verify_shares": round(float(ms_ver), 3),
+                      "combine_decrypt": round(float(ms_comb), 3)},
+        "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
+                     "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
+                     "kernel": "k_verify_shares",
+                     "work": f"{shares_here} shares x {FQMUL_PER_SHARE_VERIFY} Fq-mul x {MADS_PER_FQMUL} MAD"},
+        "check": "validity bitmap == not-corrupted; plaintexts == contributions",
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(ep, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

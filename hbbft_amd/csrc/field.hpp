@@ -27,6 +27,14 @@
 #endif
 #include "constants.hpp"
 
+// Operation counter for the roofline's algorithmic work (tools/opcount, host builds only).
+#if defined(HBX_OPCOUNT) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long hbx_opcount_fqmul;
+#define HBX_COUNT_FQMUL() (++hbx_opcount_fqmul)
+#else
+#define HBX_COUNT_FQMUL() ((void)0)
+#endif
+
 namespace hbx {
 
 struct fq {
@@ -73,6 +81,7 @@ HBX_HD fq fq_from_const(const uint32_t* c) {
 // thrash the 64 KB instruction cache and take hours to compile).  b's limbs rotate through a
 // register array so every index stays static (a dynamic b.l[i] is lowered to LDS traffic).
 HBX_HD fq fq_mul(const fq& a, const fq& b) {
+  HBX_COUNT_FQMUL();
   uint32_t t[12], bb[12];
 #pragma unroll
   for (int j = 0; j < 12; j++) {

@@ -290,4 +290,129 @@ int hbx_combine_decrypt(hbx_ctx* c, uint32_t t, uint8_t* out_blob, int32_t* stat
   return HBX_OK;
 }
 
+// ---- producer side --------------------------------------------------------------------------
+static bool scalars_canonical(const uint8_t* s32, size_t count) {
+  static const uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
+                                   0x08, 0x09, 0xa1, 0xd8, 0x05, 0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe,
+                                   0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
+  for (size_t k = 0; k < count; k++)
+    if (memcmp(s32 + 32 * k, R_BE, 32) >= 0) return false;
+  return true;
+}
+
+int hbx_public_keys(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* pk48) {
+  if (!c || !sk32 || !pk48 || n == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_public_keys: bad args");
+  if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_public_keys: scalar >= r");
+  HIPCHK(c, hipSetDevice(c->device));
+  dbuf dsk, dpk;
+  if (!dsk.ensure((size_t)n * 32) || !dpk.ensure((size_t)n * 48)) {
+    dsk.release();
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_public_keys: out of device memory");
+  }
+  int rc = HBX_OK;
+  if (hipMemcpyAsync(dsk.p, sk32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = HBX_E_DEVICE;
+  if (rc == HBX_OK) {
+    hipLaunchKernelGGL(k_public_keys, dim3((n + 63) / 64), dim3(64), 0, c->stream, dsk.as<uint8_t>(), n,
+                       dpk.as<uint8_t>());
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(pk48, dpk.p, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      rc = HBX_E_DEVICE;
+  }
+  dsk.release();
+  dpk.release();
+  return rc ? fail(c, rc, "hbx_public_keys: device error") : HBX_OK;
+}
+
+int hbx_encrypt(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off, uint32_t p,
+                const uint8_t* r32, uint8_t* u48, uint8_t* v_blob, uint8_t* w96) {
+  if (!c || !pk48 || !msg_off || !r32 || !u48 || !w96 || p == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: bad args");
+  if (!scalars_canonical(r32, p)) return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: scalar >= r");
+  for (uint32_t j = 0; j < p; j++)
+    if (msg_off[j + 1] < msg_off[j]) return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: msg_off not monotone");
+  const uint64_t total = msg_off[p];
+  if (total && (!msg_blob || !v_blob)) return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  dbuf dpkc, dpk, dst, dr, dm, doff, du, dv, dw;
+  dbuf* all[] = {&dpkc, &dpk, &dst, &dr, &dm, &doff, &du, &dv, &dw};
+  auto cleanup = [&]() { for (dbuf* b : all) b->release(); };
+  if (!dpkc.ensure(48) || !dpk.ensure(sizeof(g1a)) || !dst.ensure(4) || !dr.ensure((size_t)p * 32) ||
+      !dm.ensure(total) || !doff.ensure((size_t)(p + 1) * 8) || !du.ensure((size_t)p * 48) || !dv.ensure(total) ||
+      !dw.ensure((size_t)p * 96)) {
+    cleanup();
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_encrypt: out of device memory");
+  }
+  int rc = HBX_OK;
+  int32_t st = 0;
+  bool ok = hipMemcpyAsync(dpkc.p, pk48, 48, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+            hipMemcpyAsync(dr.p, r32, (size_t)p * 32, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+            hipMemcpyAsync(doff.p, msg_off, (size_t)(p + 1) * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+            (total == 0 || hipMemcpyAsync(dm.p, msg_blob, total, hipMemcpyHostToDevice, c->stream) == hipSuccess);
+  if (ok) {
+    hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, c->stream, dpkc.as<uint8_t>(), 1u, dpk.as<g1a>(),
+                       dst.as<int32_t>());
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(&st, dst.p, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+  }
+  if (ok && st != HBX_PT_OK) {
+    cleanup();
+    return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: public key does not decode (status %d)", st);
+  }
+  if (ok) {
+    hipLaunchKernelGGL(k_encrypt, dim3((p + 63) / 64), dim3(64), 0, c->stream, dpk.as<g1a>(), dr.as<uint8_t>(),
+                       dm.as<uint8_t>(), doff.as<uint64_t>(), p, du.as<uint8_t>(), dv.as<uint8_t>(), dw.as<uint8_t>());
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(u48, du.p, (size_t)p * 48, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         hipMemcpyAsync(w96, dw.p, (size_t)p * 96, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         (total == 0 || hipMemcpyAsync(v_blob, dv.p, total, hipMemcpyDeviceToHost, c->stream) == hipSuccess) &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+  }
+  if (!ok) rc = HBX_E_DEVICE;
+  cleanup();
+  return rc ? fail(c, rc, "hbx_encrypt: device error") : HBX_OK;
+}
+
+int hbx_decrypt_shares(hbx_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* u48, uint32_t p,
+                       uint8_t* shares48) {
+  if (!c || !sk32 || !u48 || !shares48 || n == 0 || p == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_shares: bad args");
+  if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_shares: scalar >= r");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t m = (size_t)n * p;
+  dbuf dsk, duc, du, dst, dout;
+  dbuf* all[] = {&dsk, &duc, &du, &dst, &dout};
+  auto cleanup = [&]() { for (dbuf* b : all) b->release(); };
+  if (!dsk.ensure((size_t)n * 32) || !duc.ensure((size_t)p * 48) || !du.ensure((size_t)p * sizeof(g1a)) ||
+      !dst.ensure((size_t)p * 4) || !dout.ensure(m * 48)) {
+    cleanup();
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_decrypt_shares: out of device memory");
+  }
+  std::vector<int32_t> st(p);
+  bool ok = hipMemcpyAsync(dsk.p, sk32, (size_t)n * 32, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+            hipMemcpyAsync(duc.p, u48, (size_t)p * 48, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  if (ok) {
+    hipLaunchKernelGGL(k_decompress_g1, dim3((p + 63) / 64), dim3(64), 0, c->stream, duc.as<uint8_t>(), p,
+                       du.as<g1a>(), dst.as<int32_t>());
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(st.data(), dst.p, (size_t)p * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+  }
+  for (uint32_t j = 0; ok && j < p; j++)
+    if (st[j] != HBX_PT_OK && st[j] != HBX_PT_INFINITY) {
+      cleanup();
+      return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_shares: U_%u does not decode (status %d)", j, st[j]);
+    }
+  if (ok) {
+    hipLaunchKernelGGL(k_decrypt_shares, dim3((n + 63) / 64, p), dim3(64), 0, c->stream, dsk.as<uint8_t>(), n,
+                       du.as<g1a>(), dout.as<uint8_t>());
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(shares48, dout.p, m * 48, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+  }
+  cleanup();
+  return ok ? HBX_OK : fail(c, HBX_E_DEVICE, "hbx_decrypt_shares: device error");
+}
+
 }  // extern "C"

@@ -214,4 +214,77 @@ __global__ void __launch_bounds__(64) k_keystream_xor(const uint32_t* __restrict
   for (uint64_t q = 16 * b; q < end; q++) out[off + q] = v_blob[off + q] ^ (uint8_t)ks[q - 16 * b];
 }
 
+
+// ----------------------------------------------------------------------------------------------
+// Producer side: scalar multiplications that make the
+// inputs of the verification path.  Scalars are canonical Fr values, 8 little-endian u32 limbs.
+// ----------------------------------------------------------------------------------------------
+
+// 32-byte big-endian canonical scalar -> 8 LE limbs.
+__device__ __forceinline__ void fr_from_be32(const uint8_t* b, uint32_t* k8) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = b + 28 - 4 * i;
+    k8[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+__device__ __forceinline__ g1a g1_generator() {
+  g1a g;
+  g.x = fq_from_const(G1_GEN_X);
+  g.y = fq_from_const(G1_GEN_Y);
+  g.inf = false;
+  return g;
+}
+
+// SecretKey::public_key (threshold_crypto): pk = g1 * sk, one lane per key.
+__global__ void __launch_bounds__(64) k_public_keys(const uint8_t* __restrict__ sk32, uint32_t n,
+                                                    uint8_t* __restrict__ pk48) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  fr_from_be32(sk32 + (size_t)i * 32, k);
+  const g1a pk = g1_to_affine(g1_mul_scalar(g1_from_affine(g1_generator()), k));
+  g1_compress(pk, pk48 + (size_t)i * 48);
+}
+
+// SecretKeyShare::decrypt_share_no_verify (honey_badger.rs:403): S_ji = sk_i * U_j.
+// Lane = node i, blockIdx.y = proposer j; output proposer-major like the verify input.
+__global__ void __launch_bounds__(64) k_decrypt_shares(const uint8_t* __restrict__ sk32, uint32_t n,
+                                                       const g1a* __restrict__ U, uint8_t* __restrict__ out48) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = blockIdx.y;
+  if (i >= n) return;
+  uint32_t k[8];
+  fr_from_be32(sk32 + (size_t)i * 32, k);
+  const g1a s = g1_to_affine(g1_mul_scalar(g1_from_affine(U[j]), k));
+  g1_compress(s, out48 + ((size_t)j * n + i) * 48);
+}
+
+// PublicKey::encrypt (honey_badger.rs:116) with explicit randomness r_j (threshold_crypto draws
+// it from thread_rng):  U = g1 r, V = M xor hash_bytes(pk r, |M|), W = hash_g1_g2(U, V) r.
+// One lane per message.
+__global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, const uint8_t* __restrict__ r32,
+                                                const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
+                                                uint32_t p, uint8_t* __restrict__ u48, uint8_t* __restrict__ v,
+                                                uint8_t* __restrict__ w96) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p) return;
+  uint32_t k[8];
+  fr_from_be32(r32 + (size_t)j * 32, k);
+  const g1a u = g1_to_affine(g1_mul_scalar(g1_from_affine(g1_generator()), k));
+  const g1a g = g1_to_affine(g1_mul_scalar(g1_from_affine(pk[0]), k));
+  uint8_t* uc = u48 + (size_t)j * 48;
+  g1_compress(u, uc);
+  uint8_t gc[48], d[32];
+  g1_compress(g, gc);
+  sha256_2(gc, 48, nullptr, 0, d);
+  chacha_rng rng;
+  chacha_rng_from_digest(rng, d);
+  const uint64_t o = off[j], len = off[j + 1] - o;
+  for (uint64_t q = 0; q < len; q++) v[o + q] = msg[o + q] ^ (uint8_t)chacha_next_u32(rng);
+  const g2j h = hash_g1_g2(uc, v + o, len);
+  g2_compress(g2_to_affine(g2_mul_bits(h, k, 256)), w96 + (size_t)j * 96);
+}
+
 }  // namespace hbx

@@ -38,6 +38,9 @@ EXPORTS = (
     "hbx_prepare_ciphertexts_d",
     "hbx_verify_dec_shares_d",
     "hbx_combine_decrypt_d",
+    "hbx_public_keys",
+    "hbx_encrypt",
+    "hbx_decrypt_shares",
 )
 
 _lib = None
@@ -74,6 +77,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_prepare_ciphertexts_d.argtypes = [P, P, P, P, P, u32, ctypes.c_uint64, P, P]
     lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
     lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
+    lib.hbx_public_keys.argtypes = [P, u8p, u32, u8p]
+    lib.hbx_encrypt.argtypes = [P, u8p, u8p, u64p, u32, u8p, u8p, u8p, u8p]
+    lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
     _lib = lib
     return lib
 
@@ -167,6 +173,39 @@ class Context:
         for j in range(p):
             res.append(out[int(off[j]):int(off[j + 1])].tobytes() if st[j] == HBX_OK else None)
         return res, st
+
+    # -- producer side -------------------------------------------------------
+    def public_keys(self, sk32: np.ndarray) -> np.ndarray:
+        """sk32: uint8[n, 32] big-endian canonical scalars -> uint8[n, 48] compressed g1 * sk."""
+        sk32 = np.ascontiguousarray(sk32, dtype=np.uint8)
+        n = sk32.shape[0]
+        out = np.zeros((n, 48), dtype=np.uint8)
+        self._check(self.lib.hbx_public_keys(self.h, _u8(sk32), n, _u8(out)))
+        return out
+
+    def encrypt(self, pk48: bytes, msgs: Sequence[bytes], r32: np.ndarray):
+        """PublicKey::encrypt for each message with randomness r32[j] -> list of (u48, v, w96)."""
+        p = len(msgs)
+        off = np.zeros(p + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(m) for m in msgs])
+        mb = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+        vb = np.zeros_like(mb)
+        u = np.zeros((p, 48), dtype=np.uint8)
+        w = np.zeros((p, 96), dtype=np.uint8)
+        pk = np.frombuffer(bytes(pk48), dtype=np.uint8).copy()
+        r32 = np.ascontiguousarray(r32, dtype=np.uint8)
+        self._check(self.lib.hbx_encrypt(self.h, _u8(pk), _u8(mb), off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                         p, _u8(r32), _u8(u), _u8(vb), _u8(w)))
+        return [(u[j].tobytes(), vb[int(off[j]):int(off[j + 1])].tobytes(), w[j].tobytes()) for j in range(p)]
+
+    def decrypt_shares(self, sk32: np.ndarray, u48: np.ndarray) -> np.ndarray:
+        """shares[j, i] = sk_i * U_j compressed -> uint8[p, n, 48]."""
+        sk32 = np.ascontiguousarray(sk32, dtype=np.uint8)
+        u48 = np.ascontiguousarray(u48, dtype=np.uint8)
+        n, p = sk32.shape[0], u48.shape[0]
+        out = np.zeros((p, n, 48), dtype=np.uint8)
+        self._check(self.lib.hbx_decrypt_shares(self.h, _u8(sk32), n, _u8(u48), p, _u8(out)))
+        return out
 
     # -- device API (torch tensors as HBM buffers; torch is plumbing only) -----------------------
     def prepare_ciphertexts_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_ct_valid=None, stream=None):

@@ -116,6 +116,24 @@ int hbx_verify_dec_shares_d(hbx_ctx* ctx, const uint8_t* d_shares, const uint8_t
 int hbx_combine_decrypt_d(hbx_ctx* ctx, uint32_t t, uint8_t* d_out_blob, int32_t* d_status,
                           void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Producer side.  Scalars are canonical Fr values as
+ * 32-byte big-endian strings (< r; anything else is HBX_E_INVALID_ARG).
+ *
+ * hbx_public_keys -- threshold_crypto SecretKey::public_key, pk_i = g1 * sk_i, as used by the
+ *   test key generation NetworkInfo::generate_map (src/messaging.rs:359-401).
+ * hbx_encrypt -- PublicKey::encrypt (src/honey_badger/honey_badger.rs:116) with the randomness
+ *   r_j passed in (threshold_crypto draws it from thread_rng):  U = g1 r, V = M xor
+ *   hash_bytes(pk r, |M|), W = hash_g1_g2(U, V) r.  v_blob uses the msg_off offsets.
+ * hbx_decrypt_shares -- SecretKeyShare::decrypt_share_no_verify
+ *   (src/honey_badger/honey_badger.rs:403): shares[j][i] = sk_i * U_j, proposer-major p x n x 48.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_public_keys(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, uint8_t* pk48);
+int hbx_encrypt(hbx_ctx* ctx, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off,
+                uint32_t p, const uint8_t* r32, uint8_t* u48, uint8_t* v_blob, uint8_t* w96);
+int hbx_decrypt_shares(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* u48, uint32_t p,
+                       uint8_t* shares48);
+
 #ifdef __cplusplus
 }
 #endif

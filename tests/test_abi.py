@@ -1,0 +1,56 @@
+"""The C-ABI library (hbbft_amd/libhbx.so) loads and exports every symbol include/hbx.h declares.
+No compute call is made here (no GPU in the CPU suite)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hbx.h")
+LIB = os.path.join(ROOT, "hbbft_amd", "libhbx.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    from hbbft_amd import hbx
+
+    assert names == sorted(hbx.EXPORTS)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built (run __graft_entry__.build())")
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(LIB)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    lib.hbx_version.restype = ctypes.c_char_p
+    assert lib.hbx_version().decode().startswith("hbx ")
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built")
+def test_no_silent_cpu_fallback_without_device():
+    """Without a HIP device the product must fail loudly, never compute on the CPU."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from hbbft_amd.hbx import Context, HbxError
+
+    with pytest.raises(HbxError):
+        Context(0)
+
+
+def test_shard_layout():
+    from hbbft_amd import shard
+
+    assert shard.proposer_range(256, 8, 3) == (96, 128)
+    with pytest.raises(ValueError):
+        shard.proposer_range(10, 4, 0)
+    lay = shard.slab_layout(256, 32)
+    assert lay["size"] == 256 * 32 + 32 + 128

@@ -1,0 +1,53 @@
+"""The committed golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py) agree
+with the oracle: hoisted hashes, ciphertext validity, a sample of share validities, status and
+plaintexts.  Full recomputation is done by make_golden.py; this re-checks a bounded sample."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as bls
+from oracle import threshold as tc
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(n):
+    return dict(np.load(os.path.join(GOLDEN, f"hb_epoch_n{n}.npz"), allow_pickle=False))
+
+
+@pytest.mark.parametrize("n", [4, 7])
+def test_fixture_shape(n):
+    d = _load(n)
+    p = len(d["v_off"]) - 1
+    assert d["shares"].shape == (p, n, 48) and d["expect_valid"].shape == (p, n)
+    assert int(d["t"]) == (n - 1) // 3 + 1
+    assert not d["expect_ct_valid"][0] and d["expect_ct_valid"][1:].all()
+    assert d["expect_status"][0] == -7 and d["expect_status"][-1] == -3
+
+
+@pytest.mark.parametrize("n", [4])
+def test_fixture_against_oracle(n):
+    d = _load(n)
+    off = d["v_off"]
+    p = len(off) - 1
+    pks = [bls.g1_decompress(r.tobytes()) for r in d["pk_comp"]]
+    for j in range(p):
+        u = bls.g1_decompress(d["u"][j].tobytes())
+        v = d["v_blob"][int(off[j]):int(off[j + 1])].tobytes()
+        w = bls.g2_decompress(d["w"][j].tobytes())
+        h = tc.hash_g1_g2(u, v)
+        assert bls.g2_compress(h) == d["h"][j].tobytes()
+        assert tc.ciphertext_verify((u, v, w), hash_pt=h) == bool(d["expect_ct_valid"][j])
+    # sample: proposer 1 (valid ct, one corrupted + one absent share)
+    j = 1
+    u = bls.g1_decompress(d["u"][j].tobytes())
+    v = d["v_blob"][int(off[j]):int(off[j + 1])].tobytes()
+    w = bls.g2_decompress(d["w"][j].tobytes())
+    h = bls.g2_decompress(d["h"][j].tobytes())
+    for i in range(n):
+        if not d["present"][j, i]:
+            assert not d["expect_valid"][j, i]
+            continue
+        s = bls.g1_decompress(d["shares"][j, i].tobytes())
+        assert tc.verify_decryption_share(pks[i], s, (u, v, w), hash_pt=h) == bool(d["expect_valid"][j, i])

@@ -1,0 +1,77 @@
+"""The kernels' field / curve / pairing / hash code (hbbft_amd/csrc/*.hpp, all __host__ __device__)
+compiled for the CPU by g++ (tools/hostcheck) and compared with the oracle.  This pins the GPU
+arithmetic without a GPU; the -m gpu tests then pin the kernels themselves."""
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import bls12_381 as bls
+from oracle import threshold as tc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def hc(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("hostcheck") / "libhostcheck.so")
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-o", out,
+                           os.path.join(ROOT, "tools", "hostcheck", "hostcheck.cpp")])
+    lib = ctypes.CDLL(out)
+    lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    lib.hc_hash_g1_g2.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    return lib
+
+
+def _be(x, n=48):
+    return x.to_bytes(n, "big")
+
+
+def test_fq_mul_inv(hc):
+    rnd = random.Random(1)
+    for _ in range(50):
+        a, b = rnd.randrange(bls.P), rnd.randrange(bls.P)
+        out = ctypes.create_string_buffer(48)
+        hc.hc_fq_mul(_be(a), _be(b), out)
+        assert int.from_bytes(out.raw, "big") == a * b % bls.P
+    for a in (1, 2, bls.P - 1, rnd.randrange(1, bls.P)):
+        out = ctypes.create_string_buffer(48)
+        hc.hc_fq_inv(_be(a), out)
+        assert int.from_bytes(out.raw, "big") * a % bls.P == 1
+
+
+def test_point_roundtrips(hc):
+    for k in (1, 2, 0xDEADBEEF, bls.R - 1):
+        c1 = bls.g1_compress(bls.g1_mul(bls.G1_GEN, k))
+        o1 = ctypes.create_string_buffer(48)
+        assert hc.hc_g1_roundtrip(c1, o1) == 0 and o1.raw == c1
+        c2 = bls.g2_compress(bls.g2_mul(bls.G2_GEN, k))
+        o2 = ctypes.create_string_buffer(96)
+        assert hc.hc_g2_roundtrip(c2, o2) == 0 and o2.raw == c2
+
+
+def test_pairing_check(hc):
+    a = 0x1234567890ABCDEF
+    pa = bls.g1_compress(bls.g1_mul(bls.G1_GEN, a))
+    g2 = bls.g2_compress(bls.G2_GEN)
+    qa = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a))
+    ng1 = bls.g1_compress(bls.g1_neg(bls.G1_GEN))
+    assert hc.hc_pairing_check2(pa, g2, ng1, qa) == 1          # e(aP,Q) e(-P,aQ) == 1
+    qb = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a + 1))
+    assert hc.hc_pairing_check2(pa, g2, ng1, qb) == 0
+
+
+def test_sha256_and_hash_g1_g2(hc):
+    for n in (0, 1, 55, 56, 64, 65, 200):
+        m = bytes(range(n % 251))[:n] + bytes(max(0, n - 251))
+        out = ctypes.create_string_buffer(32)
+        hc.hc_sha256(m, len(m), out)
+        assert out.raw == hashlib.sha256(m).digest()
+    u = bls.g1_mul(bls.G1_GEN, 77)
+    for v in (b"", b"x" * 64, b"y" * 65):
+        out = ctypes.create_string_buffer(96)
+        assert hc.hc_hash_g1_g2(bls.g1_compress(u), v, len(v), out) == 0
+        assert out.raw == bls.g2_compress(tc.hash_g1_g2(u, v))
