@@ -173,10 +173,12 @@ def main():
     def step(events=None):
         if events:
             events[0].record(stream)
-        ctx.prepare_ciphertexts_d(d_u, d_v, d_off, d_w, pj, maxv, d_ct_valid=d_ct_valid, stream=sh)
+        # Ciphertext::verify deferred: fused into the share-verification launch
+        ctx.prepare_ciphertexts_d(d_u, d_v, d_off, d_w, pj, maxv, d_ct_valid=None, stream=sh)
         if events:
             events[1].record(stream)
         ctx.verify_dec_shares_d(d_shares, n, pj, d_valid=d_valid, stream=sh)
+        ctx.get_ct_valid_d(d_ct_valid, stream=sh)
         if events:
             events[2].record(stream)
         ctx.combine_decrypt_d(t, d_out, d_status=d_status, stream=sh)

@@ -242,6 +242,47 @@ HBX_HDNI g2j g2_mul_bits(const g2j& p, const uint32_t* k, int nbits) {
   return acc;
 }
 
+HBX_HD g2j g2_sub(const g2j& p, const g2j& q) { return g2_add(p, g2_neg(q)); }
+
+// k * P for a 64-bit k > 0 (left-to-right double-and-add)
+HBX_HDNI g2j g2_mul_u64(const g2j& p, uint64_t k) {
+  g2j acc = p;
+  const int top = 63 - __builtin_clzll(k);
+  for (int i = top - 1; i >= 0; i--) {
+    acc = g2_dbl(acc);
+    if ((k >> i) & 1) acc = g2_add(acc, p);
+  }
+  return acc;
+}
+
+// psi(x, y) = (C1 conj(x), C2 conj(y)) on E'(Fq2), in Jacobian form (conj(Z) keeps x = X/Z^2).
+HBX_HD g2j g2_psi(const g2j& p) {
+  const fq2 c1 = fq2{fq_from_const(PSI_C1_0), fq_from_const(PSI_C1_1)};
+  const fq2 c2 = fq2{fq_from_const(PSI_C2_0), fq_from_const(PSI_C2_1)};
+  return g2j{fq2_mul(fq2_conj(p.x), c1), fq2_mul(fq2_conj(p.y), c2), fq2_conj(p.z)};
+}
+
+// h2 * P for any P on E'(Fq2) -- the value pairing 0.14's scale_by_cofactor computes with a
+// 507-bit double-and-add, here in ~4x fewer operations:
+//   Q = h_eff P by the psi formula of Budroni-Pintore / IETF hash-to-curve, h_eff = 3(x^2-1) h2;
+//   h2 P = s Q with s = (3(x^2-1))^-1 mod r = D (1 + x - x^2 - x^3), psi = [x] on G2 (Q in G2).
+HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
+  const g2j t1 = g2_neg(g2_mul_u64(P, BLS_X));  // [x] P, x = -|x|
+  g2j t2 = g2_psi(P);
+  g2j t3 = g2_psi(g2_psi(g2_dbl(P)));
+  t3 = g2_sub(t3, t2);
+  t2 = g2_add(t1, t2);
+  t2 = g2_neg(g2_mul_u64(t2, BLS_X));
+  t3 = g2_add(t3, t2);
+  t3 = g2_sub(t3, t1);
+  const g2j Q = g2_sub(t3, P);
+  const g2j q1 = g2_psi(Q);
+  const g2j q2 = g2_psi(q1);
+  const g2j q3 = g2_psi(q2);
+  const g2j Rp = g2_sub(g2_sub(g2_add(Q, q1), q2), q3);
+  return g2_mul_u64(Rp, GLS_D);
+}
+
 // zcash compressed G2 (x.c1 || x.c0) -> affine (Montgomery).  No subgroup check.
 HBX_HDNI int32_t g2_decompress(const uint8_t* b96, g2a& out) {
   const uint8_t flags = b96[0];

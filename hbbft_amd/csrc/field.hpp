@@ -75,31 +75,113 @@ HBX_HD fq fq_from_const(const uint32_t* c) {
   return r;
 }
 
-// Montgomery product, inputs <= 2p, output < 2p (no-carry CIOS; p's top limb < 2^31 - 1).
-// The outer (b-limb) loop is deliberately NOT unrolled: a fully unrolled product is ~900
-// instructions, and the Fq12 layers above would inline hundreds of them (multi-MB kernels that
-// thrash the 64 KB instruction cache and take hours to compile).  b's limbs rotate through a
-// register array so every index stays static (a dynamic b.l[i] is lowered to LDS traffic).
+// Montgomery product, inputs <= 2p, output < 2p.
+//
+// Device: Finely Integrated Product Scanning (column-wise a*b and m*p interleaved) on a 96-bit
+// accumulator (acc64, c2).  Each of the 288 partial products is ONE v_mad_u64_u32 that adds into
+// the 64-bit accumulator with its carry-out in VCC plus ONE v_addc_co_u32 into the third word --
+// no 64-bit pair construction (the compiler's lowering of `(uint64_t)a * b + t + c` spends ~2.3
+// v_mov per multiply-add on even-aligned register pairs).  p's limbs are SGPR operands.
+// Bounds: inputs < 2p and 4p < R give an output < 2p; the last column leaves no carry.
+// Host (tools/hostcheck, tools/opcount): the textbook CIOS below, same result.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HBX_MADC(acc, c2, x, y)                                                                   \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"                 \
+      : "+v"(acc), "+v"(c2)                                                                        \
+      : "v"(x), "v"(y)                                                                             \
+      : "vcc")
+// one multiply-add on each of two independent chains in one statement (hipcc pads one wait
+// state after every asm statement; pairing halves those pads)
+#define HBX_MADC2(acc, c2, x, y, acc2, c22, x2, ys2)                                              \
+  asm("v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"               \
+      "v_mad_u64_u32 %2, vcc, %6, %7, %2\n\tv_addc_co_u32 %3, vcc, 0, %3, vcc"                   \
+      : "+v"(acc), "+v"(c2), "+v"(acc2), "+v"(c22)                                                 \
+      : "v"(x), "v"(y), "v"(x2), "s"(ys2)                                                          \
+      : "vcc")
+#define HBX_MADC_S(acc, c2, x, ys)                                                                \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"                 \
+      : "+v"(acc), "+v"(c2)                                                                        \
+      : "v"(x), "s"(ys)                                                                            \
+      : "vcc")
+// 96-bit accumulator add: (acc, c2) += (x, y)
+#define HBX_ACC_ADD(acc, c2, x, y)                                                                \
+  asm("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, %3, vcc"                       \
+      : "+v"(acc), "+v"(c2)                                                                        \
+      : "v"(x), "v"(y)                                                                             \
+      : "vcc")
+// One out-of-line copy (a fully unrolled product is ~900 instructions; inlined at every call
+// site the tower code would not fit the instruction cache).  Limbs travel as 24 scalar arguments
+// so the call passes them in VGPRs (a second 12-dword aggregate would go through the stack).
+#define HBX_L12(x) x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11
+#define HBX_P12(x)                                                                                  \
+  uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6, \
+      uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
+__device__ __noinline__ fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
+  const fq a = {{HBX_L12(a)}};
+  const fq b = {{HBX_L12(b)}};
+  // two independent accumulation chains per column (a*b and m*p) so consecutive multiply-adds
+  // never depend on each other; they are merged once per column
+  uint64_t acc = 0;
+  uint32_t c2 = 0;
+  uint32_t m[12];
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 23; i++) {
+    const int jlo = i < 12 ? 0 : i - 11;
+    const int jhi = i < 12 ? i : 11;
+    uint64_t acc2 = 0;
+    uint32_t c22 = 0;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++) {
+      if (j < i) HBX_MADC2(acc, c2, a.l[j], b.l[i - j], acc2, c22, m[j], FQ_P[i - j]);
+      else HBX_MADC(acc, c2, a.l[j], b.l[i - j]);
+    }
+    // acc += acc2 (96-bit)
+    {
+      uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+      asm("v_add_co_u32 %0, vcc, %0, %3\n\tv_addc_co_u32 %1, vcc, %1, %4, vcc\n\tv_addc_co_u32 %2, vcc, %2, %5, vcc"
+          : "+v"(lo), "+v"(hi), "+v"(c2)
+          : "v"((uint32_t)acc2), "v"((uint32_t)(acc2 >> 32)), "v"(c22)
+          : "vcc");
+      acc = ((uint64_t)hi << 32) | lo;
+    }
+    if (i < 12) {
+      m[i] = (uint32_t)acc * FQ_INV;
+      HBX_MADC_S(acc, c2, m[i], FQ_P[0]);
+    } else {
+      r.l[i - 12] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)c2 << 32);
+    c2 = 0;
+  }
+  r.l[11] = (uint32_t)acc;
+  return r;
+}
 HBX_HD fq fq_mul(const fq& a, const fq& b) {
   HBX_COUNT_FQMUL();
-  uint32_t t[12], bb[12];
-#pragma unroll
-  for (int j = 0; j < 12; j++) {
-    t[j] = 0;
-    bb[j] = b.l[j];
-  }
-#pragma unroll 1
+  return fq_mul_limbs(a.l[0], a.l[1], a.l[2], a.l[3], a.l[4], a.l[5], a.l[6], a.l[7], a.l[8], a.l[9], a.l[10],
+                      a.l[11], b.l[0], b.l[1], b.l[2], b.l[3], b.l[4], b.l[5], b.l[6], b.l[7], b.l[8], b.l[9],
+                      b.l[10], b.l[11]);
+}
+#undef HBX_L12
+#undef HBX_P12
+#undef HBX_ACC_ADD
+#undef HBX_MADC
+#undef HBX_MADC_S
+#undef HBX_MADC2
+#else
+HBX_HD fq fq_mul(const fq& a, const fq& b) {
+  HBX_COUNT_FQMUL();
+  uint32_t t[12];
+  for (int j = 0; j < 12; j++) t[j] = 0;
   for (int i = 0; i < 12; i++) {
-    const uint32_t bi = bb[0];
-#pragma unroll
-    for (int k = 0; k < 11; k++) bb[k] = bb[k + 1];
+    const uint32_t bi = b.l[i];
     uint64_t s = (uint64_t)a.l[0] * bi + t[0];
     uint32_t A = (uint32_t)(s >> 32);
     const uint32_t t0 = (uint32_t)s;
     const uint32_t m = t0 * FQ_INV;
     uint64_t c = (uint64_t)m * FQ_P[0] + t0;
     uint32_t C = (uint32_t)(c >> 32);
-#pragma unroll
     for (int j = 1; j < 12; j++) {
       s = (uint64_t)a.l[j] * bi + t[j] + A;
       A = (uint32_t)(s >> 32);
@@ -110,10 +192,10 @@ HBX_HD fq fq_mul(const fq& a, const fq& b) {
     t[11] = C + A;
   }
   fq r;
-#pragma unroll
   for (int j = 0; j < 12; j++) r.l[j] = t[j];
   return r;
 }
+#endif
 
 HBX_HD fq fq_sqr(const fq& a) { return fq_mul(a, a); }
 

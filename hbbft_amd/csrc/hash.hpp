@@ -175,7 +175,7 @@ HBX_HD fq fq_rand(chacha_rng& r) {
   }
 }
 
-// G2::rand + scale_by_cofactor (full h2).
+// G2::rand + scale_by_cofactor (h2 * P; computed by g2_clear_cofactor, same point).
 HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
   for (;;) {
     const fq c0 = fq_rand(r);
@@ -187,7 +187,7 @@ HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
     if (!fq2_sqrt(rhs, y)) continue;
     // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
     if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
-    const g2j p = g2_mul_bits(g2j{x, y, fq2_one()}, G2_COFACTOR, G2_COFACTOR_BITS);
+    const g2j p = g2_clear_cofactor(g2j{x, y, fq2_one()});
     if (!g2j_is_identity(p)) return p;
   }
 }

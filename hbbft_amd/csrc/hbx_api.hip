@@ -53,13 +53,14 @@ struct hbx_ctx {
   // epoch state
   uint32_t p_ct = 0;
   dbuf U, G2pts, lines, scratch, ct_ok, ct_valid;
+  bool ct_known = false;  // ct_valid computed (else deferred into the next share verification)
   const uint8_t* d_v_blob = nullptr;  // device V blob used by the combine (caller-owned for _d)
   const uint64_t* d_v_off = nullptr;
   uint64_t max_v_len = 0;
   dbuf v_blob_own, v_off_own, u_comp_own, w_comp_own;
   // verification state
   uint32_t n_shares = 0;
-  dbuf S, valid, shares_own, present_own;
+  dbuf S, S_status, fallback, valid, shares_own, present_own;
   // combine state
   dbuf keys, status, out_own;
 };
@@ -86,6 +87,26 @@ static void pack_bits(const uint8_t* bytes, size_t n, uint8_t* bits) {
   memset(bits, 0, (n + 7) / 8);
   for (size_t k = 0; k < n; k++)
     if (bytes[k]) bits[k >> 3] |= (uint8_t)(1u << (k & 7));
+}
+
+// Pairing checks of jobs [q_first, q_last] of every proposer (q < n: shares, q == n: ciphertext).
+static int launch_pair_checks(hbx_ctx* c, hipStream_t s, uint32_t n, uint32_t p, uint32_t q_first, uint32_t q_last,
+                              const uint8_t* d_present) {
+  if (!c->fallback.ensure((size_t)p * (n + 1)))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "out of device memory (fallback flags)");
+  HIPCHK(c, hipMemsetAsync(c->fallback.p, 0, (size_t)p * (n + 1), s));
+  const uint32_t jobs = q_last - q_first + 1;
+  hipLaunchKernelGGL(k_verify_wide, dim3((jobs + WG_GROUPS - 1) / WG_GROUPS, p), dim3(WG_THREADS), 0, s,
+                     c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
+                     c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
+                     q_first, q_last, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>(), c->fallback.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  const size_t all = (size_t)p * (n + 1);
+  hipLaunchKernelGGL(k_pair_fallback, dim3((unsigned)((all + 63) / 64)), dim3(64), 0, s, c->fallback.as<uint8_t>(),
+                     c->S.as<g1a>(), c->pk.as<g1a>(), c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(),
+                     n, p, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
 }
 
 extern "C" {
@@ -118,6 +139,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   dbuf* bufs[] = {&c->pk,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
+                  &c->S_status, &c->fallback,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
@@ -164,11 +186,17 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                      c->lines.as<line_pre>(), c->scratch.as<fq2>());
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_verify_ct, dim3((p + 63) / 64), b64, 0, s, c->U.as<g1a>(), c->G2pts.as<g2a>(),
-                     c->lines.as<line_block>(), p, c->ct_ok.as<uint8_t>(), c->ct_valid.as<uint8_t>());
-  HIPCHK(c, hipGetLastError());
-  if (d_ct_valid) HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, p, hipMemcpyDeviceToDevice, s));
   c->p_ct = p;
+  c->ct_known = false;
+  if (d_ct_valid) {
+    // Ciphertext::verify now: one check per proposer (n = 0 share jobs, job 0 = the ciphertext)
+    if (!c->S.ensure(sizeof(g1a)) || !c->S_status.ensure(4) || !c->valid.ensure(16))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
+    int rc = launch_pair_checks(c, s, 0, p, 0, 0, nullptr);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, p, hipMemcpyDeviceToDevice, s));
+    c->ct_known = true;
+  }
   c->d_v_blob = d_v_blob;
   c->d_v_off = d_v_off;
   c->max_v_len = max_v_len;
@@ -193,9 +221,10 @@ int hbx_prepare_ciphertexts(hbx_ctx* c, const uint8_t* u_comp, const uint8_t* v_
   HIPCHK(c, hipMemcpyAsync(c->w_comp_own.p, w_comp, (size_t)p * 96, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->v_off_own.p, v_off, (size_t)(p + 1) * 8, hipMemcpyHostToDevice, c->stream));
   if (vbytes) HIPCHK(c, hipMemcpyAsync(c->v_blob_own.p, v_blob, vbytes, hipMemcpyHostToDevice, c->stream));
+  if (!c->ct_valid.ensure(p)) return fail(c, HBX_E_OUT_OF_MEMORY, "out of device memory");
   int rc = hbx_prepare_ciphertexts_d(c, c->u_comp_own.as<uint8_t>(), c->v_blob_own.as<uint8_t>(),
                                      c->v_off_own.as<uint64_t>(), c->w_comp_own.as<uint8_t>(), p, maxv,
-                                     nullptr, c->stream);
+                                     c->ct_valid.as<uint8_t>(), c->stream);
   if (rc) return rc;
   std::vector<uint8_t> ok(p);
   HIPCHK(c, hipMemcpyAsync(ok.data(), c->ct_valid.p, p, hipMemcpyDeviceToHost, c->stream));
@@ -212,11 +241,24 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   const size_t m = (size_t)n * p;
-  if (!c->S.ensure(m * sizeof(g1a)) || !c->valid.ensure(m))
+  if (!c->S.ensure(m * sizeof(g1a)) || !c->S_status.ensure(m * 4) || !c->valid.ensure(m))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
-  hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, d_shares, d_present,
-                     c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines.as<line_block>(),
-                     c->ct_ok.as<uint8_t>(), n, c->S.as<g1a>(), c->valid.as<uint8_t>());
+  hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, d_shares, m,
+                     c->S.as<g1a>(), c->S_status.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  // ciphertext checks (if prepare deferred them): latency-bound, p checks -> 16-lane groups
+  if (!c->ct_known) {
+    int rc = launch_pair_checks(c, s, n, p, n, n, d_present);
+    if (rc) return rc;
+    c->ct_known = true;
+  }
+  // share checks: throughput-bound, n*p checks -> one lane each
+  hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
+                     c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
+                     c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_gate_by_ct, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, c->valid.as<uint8_t>(),
+                     c->ct_valid.as<uint8_t>(), n, p);
   HIPCHK(c, hipGetLastError());
   if (d_valid) HIPCHK(c, hipMemcpyAsync(d_valid, c->valid.p, m, hipMemcpyDeviceToDevice, s));
   c->n_shares = n;
@@ -248,10 +290,18 @@ int hbx_verify_dec_shares(hbx_ctx* c, const uint8_t* shares, const uint8_t* pres
   return HBX_OK;
 }
 
+int hbx_get_ct_valid_d(hbx_ctx* c, uint8_t* d_ct_valid, void* stream) {
+  if (!c || !d_ct_valid) return fail(c, HBX_E_INVALID_ARG, "hbx_get_ct_valid_d: bad args");
+  if (c->p_ct == 0 || !c->ct_known) return fail(c, HBX_E_NO_CIPHERTEXTS, "ciphertext validity not computed yet");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, c->p_ct, hipMemcpyDeviceToDevice, pick(c, stream)));
+  return HBX_OK;
+}
+
 int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* d_status, void* stream) {
   if (!c || t == 0 || t > (uint32_t)COMBINE_MAX_T || !d_out_blob)
     return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt_d: bad args");
-  if (c->n_shares == 0 || c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares");
+  if (c->n_shares == 0 || c->p_ct == 0 || !c->ct_known) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   const uint32_t p = c->p_ct;

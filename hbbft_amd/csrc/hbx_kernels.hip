@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include "hash.hpp"
 #include "pairing.hpp"
+#include "wide.hpp"
 
 namespace hbx {
 
@@ -77,51 +78,40 @@ __global__ void __launch_bounds__(64) k_prepare_lines(const g2a* __restrict__ pt
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
   const g2a q = pts[k];
-  if (q.inf) return;
+  if (q.inf) {
+    for (int i = 0; i < MILLER_LINES; i++) {
+      lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
+      lines[(size_t)k * MILLER_LINES + i].c1 = fq2_zero();
+    }
+    return;
+  }
   g2_prepare_lines(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * 2 * MILLER_LINES);
 }
 
-// Ciphertext::verify: e(-U, H) * e(g1, W) == 1.
-__global__ void __launch_bounds__(64) k_verify_ct(const g1a* __restrict__ U, const g2a* __restrict__ G2pts,
-                                                  const line_block* __restrict__ lines, uint32_t p,
-                                                  const uint8_t* __restrict__ ct_ok, uint8_t* __restrict__ ct_valid) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= p) return;
-  bool valid = false;
-  if (ct_ok[j]) {
-    g1a nu = U[j];
-    nu.y = fq_neg(nu.y);
-    g1a g;
-    g.x = fq_from_const(G1_GEN_X);
-    g.y = fq_from_const(G1_GEN_Y);
-    g.inf = false;
-    valid = check2(lines[j].h, nu, G2pts[2 * j].inf, lines[j].w, g, G2pts[2 * j + 1].inf);
-  }
-  ct_valid[j] = valid ? 1 : 0;
-}
-
-// Share verification: lane = sender i, blockIdx.y = proposer j.
-__global__ void __launch_bounds__(64) k_verify_shares(const uint8_t* __restrict__ shares,
+// Share verification, one lane per share (lane = sender i, blockIdx.y = proposer j):
+// e(S_ji, H_j) * e(-pk_i, W_j) == 1 over the prepared lines of H_j / W_j (wave-uniform loads)
+// with one shared final exponentiation.  At N=256 one epoch is 65,536 independent checks: one
+// lane each keeps every lane of every wave busy with useful work (the throughput-optimal
+// mapping; the 16-lane group executor is kept for the latency-bound per-proposer checks).
+__global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
                                                       const uint8_t* __restrict__ present,
                                                       const g1a* __restrict__ pk, uint32_t n_keys,
                                                       const g2a* __restrict__ G2pts,
                                                       const line_block* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
-                                                      g1a* __restrict__ S, uint8_t* __restrict__ valid) {
+                                                      uint8_t* __restrict__ valid) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)j * n + i;
-  g1a s;
-  const int32_t st = g1_decompress(shares + idx * 48, s);
-  S[idx] = s;
-  bool ok = (st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && ct_ok[j] &&
-            (present == nullptr || present[idx]);
+  const int32_t st = s_status[idx];
+  const bool ok = (st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && ct_ok[j] &&
+                  (present == nullptr || present[idx]);
   bool v = false;
   if (ok) {
     g1a npk = pk[i];
     npk.y = fq_neg(npk.y);
-    v = check2(lines[j].h, s, G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf);
+    v = check2(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf);
   }
   valid[idx] = v ? 1 : 0;
 }
@@ -285,6 +275,165 @@ __global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, cons
   for (uint64_t q = 0; q < len; q++) v[o + q] = msg[o + q] ^ (uint8_t)chacha_next_u32(rng);
   const g2j h = hash_g1_g2(uc, v + o, len);
   g2_compress(g2_to_affine(g2_mul_bits(h, k, 256)), w96 + (size_t)j * 96);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Wide pairing checks: a 16-lane group per check, 8 checks of ONE
+// proposer per 128-thread block sharing that proposer's prepared lines through LDS.
+//   job q <  n : share check  e(S_jq, H_j) e(-pk_q, W_j) == 1   (verify_decryption_share)
+//   job q == n : ct check     e(-U_j, H_j) e(g1, W_j) == 1      (Ciphertext::verify)
+// Jobs with a point at infinity are flagged for k_pair_fallback (the identity cases of check2).
+// ----------------------------------------------------------------------------------------------
+constexpr int WG_GROUPS = 8;
+constexpr int WG_THREADS = WG_GROUPS * wide::G;
+constexpr int PRIV_SLOTS = prog::MAX_SCRATCH + 12 * prog::NUM_REGIONS + 4;
+constexpr int SH_SLOTS = prog::NUM_K + 16;
+constexpr int WIDE_LDS_DWORDS = (SH_SLOTS + WG_GROUPS * PRIV_SLOTS) * wide::SLOT;
+constexpr uint8_t JOB_FALLBACK = 1;
+
+__device__ __forceinline__ void put_fq(uint32_t* lds, uint32_t off, const fq& a) { wide::lds_store_fq(lds, off, a); }
+
+__global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
+    const g1a* __restrict__ S, const int32_t* __restrict__ s_status, const uint8_t* __restrict__ present,
+    const g1a* __restrict__ pk, uint32_t n_keys, const g1a* __restrict__ U, const g2a* __restrict__ G2pts,
+    const line_block* __restrict__ lines, const uint8_t* __restrict__ ct_ok, uint32_t n, uint32_t q_first,
+    uint32_t q_last, uint8_t* __restrict__ valid, uint8_t* __restrict__ ct_valid, uint8_t* __restrict__ fallback) {
+  __shared__ uint4 lds4[WIDE_LDS_DWORDS / 4];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  const int tid = threadIdx.x;
+  const int grp = tid / wide::G;
+  const int lane = tid % wide::G;
+  const uint32_t j = blockIdx.y;
+  const uint32_t q = q_first + blockIdx.x * WG_GROUPS + grp;
+  for (int t = tid; t < prog::NUM_K * wide::SLOT; t += WG_THREADS) lds[t] = prog::KCONST[t / wide::SLOT][t % wide::SLOT];
+  const uint32_t gbase = (SH_SLOTS + grp * PRIV_SLOTS) * wide::SLOT;
+  const uint32_t rbase = gbase + prog::MAX_SCRATCH * wide::SLOT;
+  const uint32_t pbase = rbase + prog::NUM_REGIONS * 12 * wide::SLOT;
+  const uint32_t lbase0 = prog::NUM_K * wide::SLOT;
+
+  // ---- job setup: decide what this group computes ----
+  const bool in_range = q <= q_last && q <= n;
+  const bool ct_job = q == n;
+  const bool qa_inf = G2pts[2 * j].inf, qb_inf = G2pts[2 * j + 1].inf;
+  bool decodable = ct_ok[j] != 0;
+  g1a PA, PB;
+  PA.inf = PB.inf = true;
+  if (in_range && decodable) {
+    if (ct_job) {
+      PA = U[j];
+      PA.y = fq_neg(PA.y);
+      PB.x = fq_from_const(G1_GEN_X);
+      PB.y = fq_from_const(G1_GEN_Y);
+      PB.inf = false;
+    } else {
+      const size_t idx = (size_t)j * n + q;
+      const int32_t st = s_status[idx];
+      decodable = (st == HBX_PT_OK || st == HBX_PT_INFINITY) && q < n_keys && (present == nullptr || present[idx]);
+      if (decodable) {
+        PA = S[idx];
+        PB = pk[q];
+        PB.y = fq_neg(PB.y);
+      }
+    }
+  }
+  const bool needs_fallback = in_range && decodable && (PA.inf || PB.inf || qa_inf || qb_inf);
+  // points: P[0..1] = P_A, P[2..3] = P_B  (any finite value for idle groups)
+  if (lane < 4) {
+    const g1a& pt = lane < 2 ? PA : PB;
+    fq v = (lane & 1) ? pt.y : pt.x;
+    if (pt.inf) v = fq_zero();
+    put_fq(lds, pbase + lane * wide::SLOT, v);
+  }
+  if (lane < 12) put_fq(lds, rbase + lane * wide::SLOT, lane == 0 ? fq_one() : fq_zero());
+  __syncthreads();
+
+  // ---- the schedule: Miller loop with line loads, then the final exponentiation ----
+  wide::bases b;
+  b.cls[prog::SCR] = gbase;
+  b.cls[prog::PT] = pbase;
+  b.cls[prog::K] = 0;
+  b.cls[prog::L] = lbase0;
+  const line_pre* la = lines[j].h;
+  const line_pre* lb = lines[j].w;
+  for (int e = 0; e < prog::SCHED_LEN; e++) {
+    const uint32_t ent = prog::SCHED[e];
+    const int line = (int)(ent >> 16) - 1;
+    if (line >= 0) {
+      const uint32_t buf = lbase0 + (line & 1) * 8 * wide::SLOT;
+      if (tid < 96) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(tid < 48 ? &la[line] : &lb[line]);
+        lds[buf + tid] = src[tid % 48];
+      }
+      b.cls[prog::L] = buf;
+      __syncthreads();
+    }
+    b.cls[prog::X] = rbase + ((ent >> 4) & 0xF) * 12 * wide::SLOT;
+    b.cls[prog::Y] = rbase + ((ent >> 8) & 0xF) * 12 * wide::SLOT;
+    b.cls[prog::O] = rbase + ((ent >> 12) & 0xF) * 12 * wide::SLOT;
+    wide::run(lds, (int)(ent & 0xF), lane, b);
+  }
+
+  // ---- result == 1 ? ----
+  bool eq = true;
+  if (lane < 12) {
+    const fq v = fq_canon(wide::lds_load_fq(lds, rbase + (prog::SCHED_RESULT_REGION * 12 + lane) * wide::SLOT));
+    const fq one = fq_one();
+#pragma unroll
+    for (int k = 0; k < 12; k++) eq = eq && v.l[k] == (lane == 0 ? one.l[k] : 0u);
+  }
+  const uint64_t bal = __ballot(eq);
+  const bool ok = ((bal >> ((tid & 63) & ~15)) & 0xFFFFull) == 0xFFFFull;
+  if (lane == 0 && in_range) {
+    const uint8_t res = (decodable && !needs_fallback && ok) ? 1 : 0;
+    if (ct_job) ct_valid[j] = res;
+    else valid[(size_t)j * n + q] = res;
+    fallback[(size_t)j * (n + 1) + q] = needs_fallback ? JOB_FALLBACK : 0;
+  }
+}
+
+// One lane per share: decompress S_ji (kept for the verification and the Lagrange combine).
+__global__ void __launch_bounds__(256) k_decompress_shares(const uint8_t* __restrict__ shares, size_t count,
+                                                           g1a* __restrict__ S, int32_t* __restrict__ status) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  g1a p;
+  status[i] = g1_decompress(shares + i * 48, p);
+  S[i] = p;
+}
+
+// Identity cases (a point at infinity on either side) that the wide kernel flagged: e(O, Q) = 1.
+__global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict__ fallback, const g1a* __restrict__ S,
+                                                      const g1a* __restrict__ pk, const g1a* __restrict__ U,
+                                                      const g2a* __restrict__ G2pts,
+                                                      const line_block* __restrict__ lines, uint32_t n, uint32_t p,
+                                                      uint8_t* __restrict__ valid, uint8_t* __restrict__ ct_valid) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (size_t)p * (n + 1) || fallback[k] != JOB_FALLBACK) return;
+  const uint32_t j = (uint32_t)(k / (n + 1)), q = (uint32_t)(k % (n + 1));
+  g1a PA, PB;
+  if (q == n) {
+    PA = U[j];
+    PA.y = fq_neg(PA.y);
+    PB.x = fq_from_const(G1_GEN_X);
+    PB.y = fq_from_const(G1_GEN_Y);
+    PB.inf = false;
+  } else {
+    PA = S[(size_t)j * n + q];
+    PB = pk[q];
+    PB.y = fq_neg(PB.y);
+  }
+  const bool v = check2(lines[j].h, PA, G2pts[2 * j].inf, lines[j].w, PB, G2pts[2 * j + 1].inf);
+  if (q == n) ct_valid[j] = v ? 1 : 0;
+  else valid[(size_t)j * n + q] = v ? 1 : 0;
+}
+
+// valid[j][i] &= ct_valid[j]: the reference never verifies shares of a ciphertext that failed
+// Ciphertext::verify (honey_badger.rs:371-376).
+__global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid, const uint8_t* __restrict__ ct_valid,
+                                                    uint32_t n, uint32_t p) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (size_t)n * p) return;
+  if (!ct_valid[k / n]) valid[k] = 0;
 }
 
 }  // namespace hbx

@@ -38,6 +38,7 @@ EXPORTS = (
     "hbx_prepare_ciphertexts_d",
     "hbx_verify_dec_shares_d",
     "hbx_combine_decrypt_d",
+    "hbx_get_ct_valid_d",
     "hbx_public_keys",
     "hbx_encrypt",
     "hbx_decrypt_shares",
@@ -77,6 +78,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_prepare_ciphertexts_d.argtypes = [P, P, P, P, P, u32, ctypes.c_uint64, P, P]
     lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
     lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
+    lib.hbx_get_ct_valid_d.argtypes = [P, P, P]
     lib.hbx_public_keys.argtypes = [P, u8p, u32, u8p]
     lib.hbx_encrypt.argtypes = [P, u8p, u8p, u64p, u32, u8p, u8p, u8p, u8p]
     lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
@@ -217,6 +219,9 @@ class Context:
         self._check(self.lib.hbx_verify_dec_shares_d(
             self.h, d_shares.data_ptr(), None if d_present is None else d_present.data_ptr(), n, p,
             None if d_valid is None else d_valid.data_ptr(), stream))
+
+    def get_ct_valid_d(self, d_ct_valid, stream=None):
+        self._check(self.lib.hbx_get_ct_valid_d(self.h, d_ct_valid.data_ptr(), stream))
 
     def combine_decrypt_d(self, t: int, d_out, d_status=None, stream=None):
         self._check(self.lib.hbx_combine_decrypt_d(

@@ -107,6 +107,9 @@ int hbx_combine_decrypt(hbx_ctx* ctx, uint32_t t, uint8_t* out_blob, int32_t* st
 /* ---------------------------------------------------------------------------------------------
  * Device-pointer / stream variants (inputs resident in HBM; nothing is copied to the host).
  *   d_valid / d_ct_valid / d_present are byte-per-item arrays.
+ * hbx_prepare_ciphertexts_d with d_ct_valid == NULL DEFERS Ciphertext::verify: the checks then run
+ * fused into the next hbx_verify_dec_shares_d launch (one more pairing check per proposer next
+ * to its n share checks), and hbx_get_ct_valid_d copies the result out afterwards.
  * ------------------------------------------------------------------------------------------- */
 int hbx_prepare_ciphertexts_d(hbx_ctx* ctx, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
                               const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
@@ -115,6 +118,7 @@ int hbx_verify_dec_shares_d(hbx_ctx* ctx, const uint8_t* d_shares, const uint8_t
                             uint32_t n, uint32_t p, uint8_t* d_valid, void* stream);
 int hbx_combine_decrypt_d(hbx_ctx* ctx, uint32_t t, uint8_t* d_out_blob, int32_t* d_status,
                           void* stream);
+int hbx_get_ct_valid_d(hbx_ctx* ctx, uint8_t* d_ct_valid, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Producer side.  Scalars are canonical Fr values as

@@ -75,3 +75,22 @@ def test_sha256_and_hash_g1_g2(hc):
         out = ctypes.create_string_buffer(96)
         assert hc.hc_hash_g1_g2(bls.g1_compress(u), v, len(v), out) == 0
         assert out.raw == bls.g2_compress(tc.hash_g1_g2(u, v))
+
+
+def test_g2_clear_cofactor_psi(hc):
+    """h2 * P by the psi / GLS route equals the full 507-bit multiplication (pairing 0.14's
+    scale_by_cofactor) for points of E'(Fq2) OUTSIDE G2."""
+    rnd = random.Random(11)
+    done = 0
+    while done < 3:
+        x = (rnd.randrange(bls.P), rnd.randrange(bls.P))
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is None:
+            continue
+        pt = (x, y)
+        assert bls.g2_mul(pt, bls.R) is not None          # not in G2
+        o1, o2 = ctypes.create_string_buffer(96), ctypes.create_string_buffer(96)
+        assert hc.hc_g2_clear_cofactor(bls.g2_compress(pt), o1) == 0
+        assert hc.hc_g2_mul_cofactor(bls.g2_compress(pt), o2) == 0
+        assert o1.raw == o2.raw == bls.g2_compress(bls.g2_mul(pt, bls.H2))
+        done += 1

@@ -38,6 +38,10 @@ int hc_pairing_check2(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, c
   g2_prepare_lines(QB, LB, scratch);
   return pairing_check2(LA, PA, LB, PB) ? 1 : 0;
 }
+int hc_g2_clear_cofactor(const uint8_t* in96, uint8_t* out96) {
+  g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
+  g2_compress(g2_to_affine(g2_clear_cofactor(g2_from_affine(p))), out96); return 0;
+}
 int hc_g2_mul_cofactor(const uint8_t* in96, uint8_t* out96) {
   g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
   g2j r = g2_mul_bits(g2_from_affine(p), G2_COFACTOR, G2_COFACTOR_BITS);
