@@ -1,0 +1,428 @@
+// Broadcast byte path on gfx950: Reed-Solomon
+// GF(2^8) coding as reed-solomon-erasure 3.1.0 defines it and the SHA-256 Merkle tree of the
+// afck/merkle.rs fork, for whole batches of broadcast instances (reference src/broadcast.rs).
+//
+// HBM layout: one instance = n shards of L bytes, contiguous ([inst][n][L]); leaf i of an
+// instance is the index byte i followed by shard i (broadcast.rs:373-377), never materialised.
+// All of it is byte/integer work: the roofline is HBM bandwidth for RS (k reads + m writes per
+// column) and the integer VALU for SHA-256 (64 rounds per 64-byte block); no MFMA.
+#pragma once
+#include "hash.hpp"
+
+namespace hbx {
+
+// ---------------------------------------------------------------------------------------------
+// GF(2^8): tables built on the host (hbx_api.hip) and staged in LDS.  log[0] = 512 (sentinel);
+// exp has 768 entries, zero from index 510 on, so exp[log a + log c] is a*c for every byte a and
+// nonzero coefficient c (zero coefficients are skipped: log = 0xFFFF).
+// ---------------------------------------------------------------------------------------------
+constexpr uint16_t GF_LOG_ZERO = 512;
+constexpr uint16_t GF_COEF_ZERO = 0xFFFF;
+constexpr int RS_OUT_CHUNK = 16;
+constexpr int RS_MAX_K = 128;
+constexpr int RS_MAX_N = 256;
+
+struct gf_tab {
+  uint16_t lg[256];
+  uint8_t ex[768];
+};
+
+__device__ __forceinline__ void gf_stage(gf_tab& T, const uint16_t* glog, const uint8_t* gexp) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) T.lg[i] = glog[i];
+  for (int i = threadIdx.x; i < 768; i += blockDim.x) T.ex[i] = gexp[i];
+}
+
+__device__ __forceinline__ uint8_t gf_mul(const gf_tab& T, uint8_t a, uint8_t b) {
+  return (a == 0 || b == 0) ? 0 : T.ex[T.lg[a] + T.lg[b]];
+}
+
+// Per-instance coding job: out rows = XOR_c coef[o][c] * in rows c  (byte columns).
+struct rs_job {
+  int32_t n_out;
+  int32_t in_idx[RS_MAX_K];
+  int32_t out_idx[RS_MAX_N];
+};
+
+// grid (ceil(L / (4 * 256)), inst); thread = 4 consecutive byte columns of one instance.
+// coef: [inst][RS_MAX_N][k] logs (GF_COEF_ZERO for 0).  Coefficient reads are wave-uniform.
+// job_stride = 0: every instance runs job 0 (encode); 1: per-instance jobs (reconstruct).
+__global__ void __launch_bounds__(256) k_rs_code(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
+                                                 uint32_t k, const rs_job* __restrict__ jobs,
+                                                 const uint16_t* __restrict__ coef, uint32_t job_stride,
+                                                 const uint16_t* __restrict__ glog, const uint8_t* __restrict__ gexp) {
+  __shared__ gf_tab T;
+  gf_stage(T, glog, gexp);
+  __syncthreads();
+  const uint32_t inst = blockIdx.y;
+  const rs_job& J = jobs[inst * job_stride];
+  const int no = J.n_out;
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (no == 0 || col >= L) return;
+  uint8_t* base = shards + (size_t)inst * inst_stride;
+  const uint16_t* cl = coef + (size_t)inst * job_stride * RS_MAX_N * k;
+  const uint32_t nb = L - col < 4 ? L - col : 4;
+  for (int o0 = 0; o0 < no; o0 += RS_OUT_CHUNK) {
+    uint32_t acc[RS_OUT_CHUNK];
+#pragma unroll
+    for (int o = 0; o < RS_OUT_CHUNK; o++) acc[o] = 0;
+    for (uint32_t c = 0; c < k; c++) {
+      const uint8_t* src = base + (size_t)J.in_idx[c] * L + col;
+      uint32_t lg4[4];
+      if (nb == 4 && ((uintptr_t)src & 3) == 0) {
+        const uint32_t d = *reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+        for (int q = 0; q < 4; q++) lg4[q] = T.lg[(d >> (8 * q)) & 0xFF];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) lg4[q] = (uint32_t)q < nb ? T.lg[src[q]] : GF_LOG_ZERO;
+      }
+#pragma unroll
+      for (int o = 0; o < RS_OUT_CHUNK; o++) {
+        if (o0 + o < no) {
+          const uint32_t lc = cl[(o0 + o) * k + c];
+          if (lc != GF_COEF_ZERO)
+            acc[o] ^= (uint32_t)T.ex[lg4[0] + lc] | ((uint32_t)T.ex[lg4[1] + lc] << 8) |
+                      ((uint32_t)T.ex[lg4[2] + lc] << 16) | ((uint32_t)T.ex[lg4[3] + lc] << 24);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < RS_OUT_CHUNK; o++) {
+      if (o0 + o < no) {
+        uint8_t* dst = base + (size_t)J.out_idx[o0 + o] * L + col;
+        if (nb == 4 && ((uintptr_t)dst & 3) == 0) {
+          *reinterpret_cast<uint32_t*>(dst) = acc[o];
+        } else {
+          for (uint32_t q = 0; q < nb; q++) dst[q] = (uint8_t)(acc[o] >> (8 * q));
+        }
+      }
+    }
+  }
+}
+
+// reconstruct_shards set-up, one block per instance (reed-solomon-erasure 3.1.0):
+// first k present shards -> invert that k x k sub-matrix of the encoding matrix (Gauss-Jordan in
+// LDS) -> job 0: rebuild missing data shards from the k sub shards; job 1: re-encode missing
+// parity shards from the (then complete) data shards.  status: 0, or HBX_E_TOO_FEW_SHARDS.
+__global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __restrict__ present, uint32_t k,
+                                                              uint32_t m, const uint8_t* __restrict__ enc,
+                                                              const uint16_t* __restrict__ glog,
+                                                              const uint8_t* __restrict__ gexp,
+                                                              rs_job* __restrict__ jobs_data,
+                                                              uint16_t* __restrict__ coef_data,
+                                                              rs_job* __restrict__ jobs_par,
+                                                              uint16_t* __restrict__ coef_par,
+                                                              int32_t* __restrict__ status) {
+  __shared__ gf_tab T;
+  __shared__ uint8_t A[RS_MAX_K][2 * RS_MAX_K];
+  __shared__ int32_t sub[RS_MAX_K];
+  __shared__ int32_t s_count, s_nmd, s_nmp, s_swap;
+  __shared__ int32_t missing_data[RS_MAX_K], missing_par[RS_MAX_N];
+  __shared__ uint8_t factor[RS_MAX_K];
+  gf_stage(T, glog, gexp);
+  const uint32_t inst = blockIdx.x;
+  const uint32_t n = k + m;
+  const uint8_t* pr = present + (size_t)inst * n;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int c = 0, nmd = 0, nmp = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      if (pr[i]) {
+        if (c < (int)k) sub[c] = (int32_t)i;
+        c++;
+      } else if (i < k) {
+        missing_data[nmd++] = (int32_t)i;
+      } else {
+        missing_par[nmp++] = (int32_t)i;
+      }
+    }
+    s_count = c;
+    s_nmd = nmd;
+    s_nmp = nmp;
+  }
+  __syncthreads();
+  rs_job& JD = jobs_data[inst];
+  rs_job& JP = jobs_par[inst];
+  if (s_count < (int)k || s_count == (int)n) {
+    if (tid == 0) {
+      JD.n_out = 0;
+      JP.n_out = 0;
+      status[inst] = s_count < (int)k ? -9 : 0;
+    }
+    return;
+  }
+  // [sub-matrix | I]
+  for (uint32_t e = tid; e < k * 2 * k; e += blockDim.x) {
+    const uint32_t r = e / (2 * k), c = e % (2 * k);
+    A[r][c] = c < k ? enc[(size_t)sub[r] * k + c] : (c - k == r ? 1 : 0);
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < k; r++) {
+    if (tid == 0) {
+      s_swap = -1;
+      if (A[r][r] == 0)
+        for (uint32_t b = r + 1; b < k; b++)
+          if (A[b][r]) {
+            s_swap = (int32_t)b;
+            break;
+          }
+    }
+    __syncthreads();
+    if (s_swap >= 0)
+      for (uint32_t c = tid; c < 2 * k; c += blockDim.x) {
+        const uint8_t t = A[r][c];
+        A[r][c] = A[s_swap][c];
+        A[s_swap][c] = t;
+      }
+    __syncthreads();
+    const uint8_t piv = A[r][r];
+    const uint8_t inv = piv ? T.ex[255 - T.lg[piv]] : 0;  // MDS: piv != 0 after the row swap
+    __syncthreads();
+    for (uint32_t c = tid; c < 2 * k; c += blockDim.x) A[r][c] = gf_mul(T, A[r][c], inv);
+    for (uint32_t i = tid; i < k; i += blockDim.x) factor[i] = A[i][r];
+    __syncthreads();
+    for (uint32_t e = tid; e < k * 2 * k; e += blockDim.x) {
+      const uint32_t i = e / (2 * k), c = e % (2 * k);
+      if (i != r && factor[i]) A[i][c] ^= gf_mul(T, factor[i], A[r][c]);
+    }
+    __syncthreads();
+  }
+  // job 0: missing data rows from the k sub shards
+  if (tid == 0) {
+    JD.n_out = s_nmd;
+    JP.n_out = s_nmp;
+    status[inst] = 0;
+  }
+  for (uint32_t c = tid; c < k; c += blockDim.x) {
+    JD.in_idx[c] = sub[c];
+    JP.in_idx[c] = (int32_t)c;
+  }
+  for (int o = tid; o < s_nmd; o += blockDim.x) JD.out_idx[o] = missing_data[o];
+  for (int o = tid; o < s_nmp; o += blockDim.x) JP.out_idx[o] = missing_par[o];
+  uint16_t* cd = coef_data + (size_t)inst * RS_MAX_N * k;
+  for (uint32_t e = tid; e < (uint32_t)s_nmd * k; e += blockDim.x) {
+    const uint32_t o = e / k, c = e % k;
+    const uint8_t v = A[missing_data[o]][k + c];
+    cd[o * k + c] = v ? T.lg[v] : GF_COEF_ZERO;
+  }
+  uint16_t* cp = coef_par + (size_t)inst * RS_MAX_N * k;
+  for (uint32_t e = tid; e < (uint32_t)s_nmp * k; e += blockDim.x) {
+    const uint32_t o = e / k, c = e % k;
+    const uint8_t v = enc[(size_t)missing_par[o] * k + c];
+    cp[o * k + c] = v ? T.lg[v] : GF_COEF_ZERO;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SHA-256 of (prefix bytes) || data[len]: one lane per message; the bulk of the data is read as
+// aligned dwords and realigned with v_alignbyte (leaves start at an index-byte offset).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint8_t msg_byte(uint32_t prefix, int plen, const uint8_t* data, uint64_t len, uint64_t q) {
+  if (q < (uint64_t)plen) return (uint8_t)(prefix >> (8 * q));
+  q -= plen;
+  return q < len ? data[q] : 0;
+}
+
+__device__ void sha256_prefixed(uint32_t prefix, int plen, const uint8_t* data, uint64_t len, uint32_t* h8) {
+  sha256_state s;
+  sha256_init(s);
+  const uint64_t total = (uint64_t)plen + len;
+  const uint64_t nblocks = (total + 9 + 63) / 64;
+  for (uint64_t blk = 0; blk < nblocks; blk++) {
+    uint32_t w[16];
+    const uint64_t b0 = blk * 64;
+    if (b0 >= (uint64_t)plen && b0 + 64 <= total) {
+      // fast path: the whole block is data; 17 aligned dwords cover it
+      const uint8_t* p = data + (b0 - plen);
+      const uintptr_t a = (uintptr_t)p;
+      const uint32_t* pa = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3);
+      uint32_t d[17];
+      const int nd = sh ? 17 : 16;
+#pragma unroll
+      for (int i = 0; i < 17; i++) d[i] = i < nd ? pa[i] : 0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = bswap32(__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh));
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < 16; i++) {
+        uint32_t word = 0;
+        for (int q = 0; q < 4; q++) {
+          const uint64_t pos = b0 + 4 * i + q;
+          uint8_t byte;
+          if (pos < total) byte = msg_byte(prefix, plen, data, len, pos);
+          else if (pos == total) byte = 0x80;
+          else if (pos >= nblocks * 64 - 8) byte = (uint8_t)((total * 8) >> (8 * (nblocks * 64 - 1 - pos)));
+          else byte = 0;
+          word = (word << 8) | byte;
+        }
+        w[i] = word;
+      }
+    }
+    sha256_compress(s, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) h8[i] = s.h[i];
+}
+
+// node = SHA-256(0x01 || left || right) on big-endian word digests (2 blocks)
+__device__ void sha256_node(const uint32_t* l8, const uint32_t* r8, uint32_t* out8) {
+  sha256_state s;
+  sha256_init(s);
+  uint32_t w[16];
+  // bytes: 01 | L(32) | R(32) | 80 | zeros | len=65*8
+  w[0] = 0x01000000u | (l8[0] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[i] = (l8[i - 1] << 24) | (l8[i] >> 8);
+  w[8] = (l8[7] << 24) | (r8[0] >> 8);
+#pragma unroll
+  for (int i = 9; i < 16; i++) w[i] = (r8[i - 9] << 24) | (r8[i - 8] >> 8);
+  sha256_compress(s, w);
+  w[0] = (r8[7] << 24) | 0x00800000u;
+#pragma unroll
+  for (int i = 1; i < 15; i++) w[i] = 0;
+  w[15] = 65 * 8;
+  sha256_compress(s, w);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out8[i] = s.h[i];
+}
+
+// Leaf hashes of the index-prefixed shards: leaf(i) = SHA-256(0x00 || i || shard_i).
+// grid (ceil(n/64), inst); out: u32[inst][n][8] (digest words, big-endian order).
+__global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict__ shards, size_t inst_stride,
+                                                      uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t inst = blockIdx.y;
+  if (i >= n) return;
+  uint32_t h[8];
+  sha256_prefixed((i & 0xFF) << 8, 2, shards + (size_t)inst * inst_stride + (size_t)i * L, L, h);
+  uint32_t* o = leaf_hash + ((size_t)inst * n + i) * 8;
+#pragma unroll
+  for (int q = 0; q < 8; q++) o[q] = h[q];
+}
+
+// MerkleTree::from_vec levels (pairs left to right, odd trailing node promoted): one block per
+// instance, the level in LDS.  roots: u8[inst][32].
+__global__ void __launch_bounds__(128) k_merkle_tree(const uint32_t* __restrict__ leaf_hash, uint32_t n,
+                                                     uint8_t* __restrict__ roots) {
+  __shared__ uint32_t lvl[2][RS_MAX_N][8];
+  const uint32_t inst = blockIdx.x;
+  for (uint32_t e = threadIdx.x; e < n * 8; e += blockDim.x) lvl[0][e / 8][e % 8] = leaf_hash[(size_t)inst * n * 8 + e];
+  __syncthreads();
+  uint32_t cnt = n;
+  int cur = 0;
+  while (cnt > 1) {
+    const uint32_t nxt = (cnt + 1) / 2;
+    for (uint32_t j = threadIdx.x; j < nxt; j += blockDim.x) {
+      if (2 * j + 1 < cnt) {
+        sha256_node(lvl[cur][2 * j], lvl[cur][2 * j + 1], lvl[cur ^ 1][j]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++) lvl[cur ^ 1][j][q] = lvl[cur][2 * j][q];
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+    cnt = nxt;
+  }
+  if (threadIdx.x < 32) {
+    const uint32_t wv = lvl[cur][0][threadIdx.x / 4];
+    roots[(size_t)inst * 32 + threadIdx.x] = (uint8_t)(wv >> (8 * (3 - threadIdx.x % 4)));
+  }
+}
+
+// Broadcast::validate_proof (broadcast.rs:555-575) over a batch of proofs:
+//   Proof::validate(root): root == lemma[0].node_hash == the proof's root_hash, every
+//   lemma[k].node_hash == H(01 || left || right) of its child and sibling, and the leaf lemma's
+//   hash == SHA-256(0x00 || value); then value[0] == sender index == Proof::index(count).
+// Per proof j: value = values + j * vlen (the index byte first), depth[j] <= 16,
+// nodes = node_hash + j * 17 * 32 (root first, leaf hash last), sibs = sib_hash + j * 16 * 32,
+// sides bit k set = sibling at level k is on the LEFT (merkle.rs Positioned::Left).
+__global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restrict__ values, uint32_t vlen,
+                                                        const uint8_t* __restrict__ node_hash,
+                                                        const uint8_t* __restrict__ sib_hash,
+                                                        const uint32_t* __restrict__ sides,
+                                                        const uint32_t* __restrict__ depth,
+                                                        const uint8_t* __restrict__ root_hash,
+                                                        const uint32_t* __restrict__ sender, uint32_t count,
+                                                        uint32_t nproofs, uint8_t* __restrict__ valid) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nproofs) return;
+  const uint32_t d = depth[j];
+  const uint8_t* nodes = node_hash + (size_t)j * 17 * 32;
+  const uint8_t* sibs = sib_hash + (size_t)j * 16 * 32;
+  const uint8_t* val = values + (size_t)j * vlen;
+  bool ok = d <= 16 && vlen >= 1;
+  for (int q = 0; q < 32 && ok; q++) ok = root_hash[(size_t)j * 32 + q] == nodes[q];
+  auto be8 = [](const uint8_t* p, uint32_t* w) {
+    for (int q = 0; q < 8; q++)
+      w[q] = ((uint32_t)p[4 * q] << 24) | ((uint32_t)p[4 * q + 1] << 16) | ((uint32_t)p[4 * q + 2] << 8) | p[4 * q + 3];
+  };
+  uint32_t h[8], want[8], a[8], b[8];
+  if (ok) {
+    sha256_prefixed(0, 1, val, vlen, h);
+    be8(nodes + (size_t)d * 32, want);
+    for (int q = 0; q < 8; q++) ok = ok && h[q] == want[q];
+  }
+  for (uint32_t lv = 0; lv < d && ok; lv++) {
+    be8(sibs + (size_t)lv * 32, a);
+    be8(nodes + (size_t)(lv + 1) * 32, b);
+    if ((sides[j] >> lv) & 1) sha256_node(a, b, h);
+    else sha256_node(b, a, h);
+    be8(nodes + (size_t)lv * 32, want);
+    for (int q = 0; q < 8; q++) ok = ok && h[q] == want[q];
+  }
+  // Proof::index(count) from the Left/Right path
+  uint32_t idx = 0, c = count;
+  for (uint32_t lv = 0; lv < d; lv++) {
+    const uint32_t left = c > 1 ? 1u << (31 - __clz(c - 1)) : 1u;
+    if ((sides[j] >> lv) & 1) {
+      idx += left;
+      c -= left;
+    } else {
+      c = left;
+    }
+  }
+  ok = ok && val[0] == sender[j] && idx == val[0];
+  valid[j] = ok ? 1 : 0;
+}
+
+// glue_shards (broadcast.rs:697-707) of instances whose root matched: value = the first k
+// shards concatenated, BE u32 length, then that many bytes (fewer if the data runs out).
+// One block per instance.  status in/out: 0 ok (-> HBX_E_NO_PAYLOAD if fewer than 4 bytes).
+__global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards, size_t inst_stride, uint32_t k,
+                                              uint32_t L, uint8_t* __restrict__ out, size_t out_stride,
+                                              uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
+  const uint32_t inst = blockIdx.x;
+  if (status[inst] != 0) {
+    if (threadIdx.x == 0) out_len[inst] = 0;
+    return;
+  }
+  const uint8_t* base = shards + (size_t)inst * inst_stride;  // shards 0..k-1 are contiguous
+  const uint64_t total = (uint64_t)k * L;
+  if (total < 4) {
+    if (threadIdx.x == 0) {
+      status[inst] = -11;
+      out_len[inst] = 0;
+    }
+    return;
+  }
+  const uint64_t want = ((uint64_t)base[0] << 24) | ((uint64_t)base[1] << 16) | ((uint64_t)base[2] << 8) | base[3];
+  const uint64_t len = want < total - 4 ? want : total - 4;
+  for (uint64_t q = threadIdx.x; q < len; q += blockDim.x) out[(size_t)inst * out_stride + q] = base[4 + q];
+  if (threadIdx.x == 0) out_len[inst] = len;
+}
+
+// status = root(inst) == expected ? status : HBX_E_ROOT_MISMATCH
+__global__ void k_root_check(const uint8_t* __restrict__ roots, const uint8_t* __restrict__ expect, uint32_t inst,
+                             int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= inst || status[i] != 0) return;
+  bool eq = true;
+  for (int q = 0; q < 32; q++) eq = eq && roots[(size_t)i * 32 + q] == expect[(size_t)i * 32 + q];
+  if (!eq) status[i] = -10;
+}
+
+}  // namespace hbx

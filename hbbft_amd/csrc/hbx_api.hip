@@ -8,10 +8,12 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/hbx.h"
 #include "hbx_kernels.hip"
+#include "broadcast.hpp"
 
 using namespace hbx;
 
@@ -63,6 +65,10 @@ struct hbx_ctx {
   dbuf S, S_status, fallback, valid, shares_own, present_own;
   // combine state
   dbuf keys, status, out_own;
+  // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
+  dbuf gf_log, gf_exp;
+  uint32_t rs_k = 0, rs_m = 0;
+  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, roots;
 };
 
 static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
@@ -109,6 +115,136 @@ static int launch_pair_checks(hbx_ctx* c, hipStream_t s, uint32_t n, uint32_t p,
   return HBX_OK;
 }
 
+// ---- broadcast: host-side set-up (ReedSolomon::new; tables and matrices only, no shard data) ----
+struct gf_host {
+  uint16_t lg[256];
+  uint8_t ex[768];
+  uint8_t mul(uint8_t a, uint8_t b) const { return (a == 0 || b == 0) ? 0 : ex[lg[a] + lg[b]]; }
+  uint8_t inv(uint8_t a) const { return ex[255 - lg[a]]; }
+  uint8_t pow(uint8_t a, uint32_t n) const {  // galois_8::exp, 0^0 = 1
+    if (n == 0) return 1;
+    if (a == 0) return 0;
+    return ex[(lg[a] * n) % 255];
+  }
+};
+
+static const gf_host& gf() {
+  static gf_host g = [] {
+    gf_host t{};
+    uint32_t x = 1;
+    for (int i = 0; i < 768; i++) t.ex[i] = 0;
+    for (int i = 0; i < 255; i++) {
+      t.ex[i] = (uint8_t)x;
+      t.ex[i + 255] = (uint8_t)x;
+      t.lg[x] = (uint16_t)i;
+      x <<= 1;
+      if (x & 0x100) x ^= 0x11D;
+    }
+    t.lg[0] = GF_LOG_ZERO;
+    return t;
+  }();
+  return g;
+}
+
+// Encoding matrix V * inverse(V[0..k]) with V[r][c] = r^c ((k + m) x k, reed-solomon-erasure 3.1.0).
+static bool rs_matrix(uint32_t k, uint32_t m, std::vector<uint8_t>& out) {
+  const gf_host& g = gf();
+  const uint32_t n = k + m;
+  std::vector<uint8_t> V(n * k), A(k * 2 * k);
+  for (uint32_t r = 0; r < n; r++)
+    for (uint32_t c = 0; c < k; c++) V[r * k + c] = g.pow((uint8_t)r, c);
+  for (uint32_t r = 0; r < k; r++)
+    for (uint32_t c = 0; c < 2 * k; c++) A[r * 2 * k + c] = c < k ? V[r * k + c] : (c - k == r ? 1 : 0);
+  for (uint32_t r = 0; r < k; r++) {
+    if (A[r * 2 * k + r] == 0) {
+      uint32_t b = r + 1;
+      while (b < k && A[b * 2 * k + r] == 0) b++;
+      if (b == k) return false;
+      for (uint32_t c = 0; c < 2 * k; c++) std::swap(A[r * 2 * k + c], A[b * 2 * k + c]);
+    }
+    const uint8_t inv = g.inv(A[r * 2 * k + r]);
+    for (uint32_t c = 0; c < 2 * k; c++) A[r * 2 * k + c] = g.mul(A[r * 2 * k + c], inv);
+    for (uint32_t i = 0; i < k; i++) {
+      const uint8_t f = A[i * 2 * k + r];
+      if (i == r || !f) continue;
+      for (uint32_t c = 0; c < 2 * k; c++) A[i * 2 * k + c] ^= g.mul(f, A[r * 2 * k + c]);
+    }
+  }
+  out.assign(n * k, 0);
+  for (uint32_t r = 0; r < n; r++)
+    for (uint32_t c = 0; c < k; c++) {
+      uint8_t acc = 0;
+      for (uint32_t q = 0; q < k; q++) acc ^= g.mul(V[r * k + q], A[q * 2 * k + k + c]);
+      out[r * k + c] = acc;
+    }
+  return true;
+}
+
+static int rs_setup(hbx_ctx* c, uint32_t k, uint32_t m, hipStream_t s) {
+  if (k == 0 || k > (uint32_t)RS_MAX_K || k + m > (uint32_t)RS_MAX_N)
+    return fail(c, HBX_E_INVALID_ARG, "rs: need 1 <= k <= %d and k + m <= %d (k=%u m=%u)", RS_MAX_K, RS_MAX_N, k, m);
+  if (!c->gf_log.p) {
+    if (!c->gf_log.ensure(512) || !c->gf_exp.ensure(768)) return fail(c, HBX_E_OUT_OF_MEMORY, "rs: tables");
+    HIPCHK(c, hipMemcpyAsync(c->gf_log.p, gf().lg, 512, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->gf_exp.p, gf().ex, 768, hipMemcpyHostToDevice, s));
+  }
+  if (c->rs_k == k && c->rs_m == m) return HBX_OK;
+  std::vector<uint8_t> M;
+  if (m > 0 && !rs_matrix(k, m, M)) return fail(c, HBX_E_INVALID_ARG, "rs: singular Vandermonde block");
+  if (m == 0) M.assign((size_t)k * k, 0);
+  rs_job job{};
+  job.n_out = (int32_t)m;
+  for (uint32_t q = 0; q < k; q++) job.in_idx[q] = (int32_t)q;
+  for (uint32_t o = 0; o < m; o++) job.out_idx[o] = (int32_t)(k + o);
+  std::vector<uint16_t> coef((size_t)RS_MAX_N * k, GF_COEF_ZERO);
+  for (uint32_t o = 0; o < m; o++)
+    for (uint32_t q = 0; q < k; q++) {
+      const uint8_t v = M[(size_t)(k + o) * k + q];
+      coef[(size_t)o * k + q] = v ? gf().lg[v] : GF_COEF_ZERO;
+    }
+  if (!c->rs_enc.ensure(M.size()) || !c->rs_enc_job.ensure(sizeof(rs_job)) || !c->rs_enc_coef.ensure(coef.size() * 2))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "rs: matrix");
+  HIPCHK(c, hipMemcpyAsync(c->rs_enc.p, M.data(), M.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->rs_enc_job.p, &job, sizeof(rs_job), hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->rs_enc_coef.p, coef.data(), coef.size() * 2, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipStreamSynchronize(s));  // host staging buffers die at return
+  c->rs_k = k;
+  c->rs_m = m;
+  return HBX_OK;
+}
+
+static int rs_reconstruct(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, uint32_t inst, uint32_t k,
+                          uint32_t m, uint32_t L, int32_t* d_status, hipStream_t s) {
+  const size_t stride = (size_t)(k + m) * L;
+  if (!c->rs_jobs_d.ensure((size_t)inst * sizeof(rs_job)) || !c->rs_jobs_p.ensure((size_t)inst * sizeof(rs_job)) ||
+      !c->rs_coef_d.ensure((size_t)inst * RS_MAX_N * k * 2) || !c->rs_coef_p.ensure((size_t)inst * RS_MAX_N * k * 2))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "rs_reconstruct: out of device memory");
+  hipLaunchKernelGGL(k_rs_setup_reconstruct, dim3(inst), dim3(256), 0, s, d_present, k, m, c->rs_enc.as<uint8_t>(),
+                     c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>(), c->rs_jobs_d.as<rs_job>(),
+                     c->rs_coef_d.as<uint16_t>(), c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(), d_status);
+  HIPCHK(c, hipGetLastError());
+  const dim3 grid((L + 1023) / 1024, inst);
+  hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_d.as<rs_job>(),
+                     c->rs_coef_d.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_p.as<rs_job>(),
+                     c->rs_coef_p.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* d_roots,
+                        hipStream_t s) {
+  if (n == 0 || n > (uint32_t)RS_MAX_N) return fail(c, HBX_E_INVALID_ARG, "merkle: need 1 <= n <= 256");
+  if (!c->leaf_hash.ensure((size_t)inst * n * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: leaf hashes");
+  hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
+                     c->leaf_hash.as<uint32_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots);
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
 extern "C" {
 
 const char* hbx_version(void) { return "hbx 0.1.0 gfx950"; }
@@ -140,7 +276,9 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback,
-                  &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own};
+                  &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
+                  &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef,
+                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -287,6 +425,75 @@ int hbx_verify_dec_shares(hbx_ctx* c, const uint8_t* shares, const uint8_t* pres
   HIPCHK(c, hipMemcpyAsync(v.data(), c->valid.p, m, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (valid_bits) pack_bits(v.data(), m, valid_bits);
+  return HBX_OK;
+}
+
+int hbx_rs_encode_d(hbx_ctx* c, uint8_t* d_shards, uint32_t inst, uint32_t k, uint32_t m, uint32_t L, void* stream) {
+  if (!c || !d_shards || inst == 0 || L == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_rs_encode_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (m == 0) return HBX_OK;  // Coding::Trivial
+  int rc = rs_setup(c, k, m, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, L, k,
+                     c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(), 0u, c->gf_log.as<uint16_t>(),
+                     c->gf_exp.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+int hbx_rs_reconstruct_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, uint32_t inst, uint32_t k,
+                         uint32_t m, uint32_t L, int32_t* d_status, void* stream) {
+  if (!c || !d_shards || !d_present || !d_status || inst == 0 || L == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_rs_reconstruct_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  int rc = rs_setup(c, k, m, s);
+  if (rc) return rc;
+  return rs_reconstruct(c, d_shards, d_present, inst, k, m, L, d_status, s);
+}
+
+int hbx_merkle_roots_d(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* d_roots,
+                       void* stream) {
+  if (!c || !d_shards || !d_roots || inst == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_roots_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  return merkle_roots(c, d_shards, inst, n, L, d_roots, pick(c, stream));
+}
+
+int hbx_merkle_validate_d(hbx_ctx* c, const uint8_t* d_values, uint32_t vlen, const uint8_t* d_node_hash,
+                          const uint8_t* d_sib_hash, const uint32_t* d_sides, const uint32_t* d_depth,
+                          const uint8_t* d_root, const uint32_t* d_sender, uint32_t count, uint32_t nproofs,
+                          uint8_t* d_valid, void* stream) {
+  if (!c || !d_values || !d_node_hash || !d_sib_hash || !d_sides || !d_depth || !d_root || !d_sender || !d_valid ||
+      nproofs == 0 || vlen == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_validate_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_merkle_validate, dim3((nproofs + 63) / 64), dim3(64), 0, pick(c, stream), d_values, vlen,
+                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid);
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, const uint8_t* d_root_expect,
+                           uint32_t inst, uint32_t k, uint32_t m, uint32_t L, uint8_t* d_out, uint64_t out_stride,
+                           uint64_t* d_out_len, int32_t* d_status, void* stream) {
+  if (!c || !d_shards || !d_present || !d_root_expect || !d_out || !d_out_len || !d_status || inst == 0 || L == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  int rc = rs_setup(c, k, m, s);
+  if (rc) return rc;
+  rc = rs_reconstruct(c, d_shards, d_present, inst, k, m, L, d_status, s);
+  if (rc) return rc;
+  if (!c->roots.ensure((size_t)inst * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "decode: roots");
+  rc = merkle_roots(c, d_shards, inst, k + m, L, c->roots.as<uint8_t>(), s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_root_check, dim3((inst + 63) / 64), dim3(64), 0, s, c->roots.as<uint8_t>(), d_root_expect, inst,
+                     d_status);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_glue, dim3(inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, k, L, d_out,
+                     (size_t)out_stride, d_out_len, d_status);
+  HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
 

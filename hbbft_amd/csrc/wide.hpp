@@ -107,16 +107,33 @@ __device__ __forceinline__ fq acc_reduce(acc13 acc, int K) {
   return r;
 }
 
-// sum of terms [t0, t1) of instruction `ins` (term words read from the constant table: a
-// register array indexed by a loop counter would live in scratch).  Returns the raw sum and S.
-__device__ __forceinline__ acc13 sum_terms(const uint32_t* lds, const bases& b, const uint32_t* ins, int t0, int t1,
-                                           int& S) {
-  acc13 acc;
+// Instruction words live in registers (loaded once per round, prefetched a round ahead); the
+// term loop is unrolled so every word index is static.
+struct insn {
+  uint4 w[4];
+};
+__device__ __forceinline__ uint32_t insn_word(const insn& I, int k) {
+  const uint4 v = I.w[k >> 2];
+  return (k & 3) == 0 ? v.x : (k & 3) == 1 ? v.y : (k & 3) == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ insn load_insn(uint32_t idx) {
+  insn I;
+  const uint4* p = reinterpret_cast<const uint4*>(prog::INSNS[idx]);
 #pragma unroll
-  for (int i = 0; i < 13; i++) acc.l[i] = 0;
-  S = 0;
-  for (int t = t0; t < t1; t++) {
-    const uint32_t term = ins[1 + t];
+  for (int q = 0; q < 4; q++) I.w[q] = p[q];
+  return I;
+}
+
+// Raw sums of the A terms [0, na) and B terms [na, na + nb); S = sum |c| of each.
+__device__ __forceinline__ void sum_terms(const uint32_t* lds, const bases& b, const insn& I, int na, int nb,
+                                          acc13& ra, int& SA, acc13& rb, int& SB) {
+#pragma unroll
+  for (int i = 0; i < 13; i++) ra.l[i] = rb.l[i] = 0;
+  SA = SB = 0;
+#pragma unroll
+  for (int t = 0; t < 15; t++) {
+    if (t < na + nb) {
+    const uint32_t term = insn_word(I, 1 + t);
     fq v = lds_load_fq(lds, slot_off(b, (term >> 16) & 0xF, term & 0xFFFF));
     const int c = (int)(int8_t)(term >> 24);
     if (c < 0) {  // 2p - v
@@ -129,10 +146,15 @@ __device__ __forceinline__ acc13 sum_terms(const uint32_t* lds, const bases& b, 
       }
     }
     const int m = c < 0 ? -c : c;
-    S += m;
-    for (int q = 0; q < m; q++) acc_add(acc, v.l);
+    if (t < na) {
+      SA += m;
+      for (int q = 0; q < m; q++) acc_add(ra, v.l);
+    } else {
+      SB += m;
+      for (int q = 0; q < m; q++) acc_add(rb, v.l);
+    }
+    }
   }
-  return acc;
 }
 
 __device__ __forceinline__ int ladder_steps(int S) { return S <= 1 ? 0 : 32 - __clz(S - 1); }
@@ -163,23 +185,26 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ void run(uint32_t* lds, int prog, int lane, const bases& b) {
   const uint32_t s0 = prog::PROG_STAGES[prog][0];
   const uint32_t ns = prog::PROG_STAGES[prog][1];
+  uint32_t cnt = prog::STAGES[s0][1];
+  insn cur = load_insn(prog::STAGES[s0][0] + ((uint32_t)lane < cnt ? lane : 0));
   for (uint32_t s = s0; s < s0 + ns; s++) {
-    const uint32_t first = prog::STAGES[s][0];
-    const uint32_t cnt = prog::STAGES[s][1];
     const bool act = (uint32_t)lane < cnt;
+    // prefetch the next round's instruction while this one computes
+    const uint32_t ncnt = s + 1 < s0 + ns ? prog::STAGES[s + 1][1] : 0;
+    const insn nxt = load_insn(s + 1 < s0 + ns ? prog::STAGES[s + 1][0] + ((uint32_t)lane < ncnt ? lane : 0)
+                                               : prog::STAGES[s][0]);
     fq r = fq_zero();
     uint32_t dst = 0;
     if (act) {
-      const uint32_t* ins = prog::INSNS[first + lane];
-      const uint32_t hdr = ins[0];
+      const uint32_t hdr = cur.w[0].x;
       const uint32_t op = hdr & 0xF, na = (hdr >> 4) & 0xF, nb = (hdr >> 8) & 0xF;
       dst = slot_off(b, (hdr >> 12) & 0xF, hdr >> 16);
+      acc13 ra, rb;
       int SA, SB;
-      const acc13 ra = sum_terms(lds, b, ins, 0, (int)na, SA);
+      sum_terms(lds, b, cur, (int)na, (int)nb, ra, SA, rb, SB);
       if (op == 0) {
         // MUL: A may stay raw while < 2^383 (S <= 2: 2 * 2p < 2^383; then A*B < p R and the product < 2p);
         // B must be < 2p
-        const acc13 rb = sum_terms(lds, b, ins, (int)na, (int)(na + nb), SB);
         const fq fa = acc_reduce(ra, SA <= 2 ? 0 : ladder_steps(SA));
         const fq fb = acc_reduce(rb, ladder_steps(SB));
         r = fq_mul(fa, fb);
@@ -192,6 +217,8 @@ __device__ __forceinline__ void run(uint32_t* lds, int prog, int lane, const bas
     __builtin_amdgcn_wave_barrier();
     if (act) lds_store_fq(lds, dst, r);
     wave_sync();
+    cur = nxt;
+    cnt = ncnt;
   }
 }
 

@@ -24,6 +24,9 @@ HBX_E_NO_KEYS = -5
 HBX_E_NO_CIPHERTEXTS = -6
 HBX_E_INVALID_CIPHERTEXT = -7
 HBX_E_OUT_OF_MEMORY = -8
+HBX_E_TOO_FEW_SHARDS = -9
+HBX_E_ROOT_MISMATCH = -10
+HBX_E_NO_PAYLOAD = -11
 
 # Every symbol include/hbx.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -42,6 +45,11 @@ EXPORTS = (
     "hbx_public_keys",
     "hbx_encrypt",
     "hbx_decrypt_shares",
+    "hbx_rs_encode_d",
+    "hbx_rs_reconstruct_d",
+    "hbx_merkle_roots_d",
+    "hbx_merkle_validate_d",
+    "hbx_broadcast_decode_d",
 )
 
 _lib = None
@@ -79,6 +87,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
     lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
     lib.hbx_get_ct_valid_d.argtypes = [P, P, P]
+    lib.hbx_rs_encode_d.argtypes = [P, P, u32, u32, u32, u32, P]
+    lib.hbx_rs_reconstruct_d.argtypes = [P, P, P, u32, u32, u32, u32, P, P]
+    lib.hbx_merkle_roots_d.argtypes = [P, P, u32, u32, u32, P, P]
+    lib.hbx_merkle_validate_d.argtypes = [P, P, u32, P, P, P, P, P, P, u32, u32, P, P]
+    lib.hbx_broadcast_decode_d.argtypes = [P, P, P, P, u32, u32, u32, u32, P, ctypes.c_uint64, P, P, P]
     lib.hbx_public_keys.argtypes = [P, u8p, u32, u8p]
     lib.hbx_encrypt.argtypes = [P, u8p, u8p, u64p, u32, u8p, u8p, u8p, u8p]
     lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
@@ -219,6 +232,35 @@ class Context:
         self._check(self.lib.hbx_verify_dec_shares_d(
             self.h, d_shares.data_ptr(), None if d_present is None else d_present.data_ptr(), n, p,
             None if d_valid is None else d_valid.data_ptr(), stream))
+
+    # -- broadcast (torch tensors as HBM buffers) ------------------------------------------------
+    def rs_encode_d(self, d_shards, k: int, m: int, stream=None):
+        """d_shards: uint8[inst, k + m, L] (parity rows overwritten)."""
+        inst, n, L = d_shards.shape
+        assert n == k + m
+        self._check(self.lib.hbx_rs_encode_d(self.h, d_shards.data_ptr(), inst, k, m, L, stream))
+
+    def rs_reconstruct_d(self, d_shards, d_present, d_status, k: int, m: int, stream=None):
+        inst, n, L = d_shards.shape
+        self._check(self.lib.hbx_rs_reconstruct_d(self.h, d_shards.data_ptr(), d_present.data_ptr(), inst, k, m, L,
+                                                  d_status.data_ptr(), stream))
+
+    def merkle_roots_d(self, d_shards, d_roots, stream=None):
+        inst, n, L = d_shards.shape
+        self._check(self.lib.hbx_merkle_roots_d(self.h, d_shards.data_ptr(), inst, n, L, d_roots.data_ptr(), stream))
+
+    def merkle_validate_d(self, d_values, d_nodes, d_sibs, d_sides, d_depth, d_root, d_sender, count: int, d_valid,
+                          stream=None):
+        nproofs, vlen = d_values.shape
+        self._check(self.lib.hbx_merkle_validate_d(
+            self.h, d_values.data_ptr(), vlen, d_nodes.data_ptr(), d_sibs.data_ptr(), d_sides.data_ptr(),
+            d_depth.data_ptr(), d_root.data_ptr(), d_sender.data_ptr(), count, nproofs, d_valid.data_ptr(), stream))
+
+    def broadcast_decode_d(self, d_shards, d_present, d_root, k: int, m: int, d_out, d_out_len, d_status, stream=None):
+        inst, n, L = d_shards.shape
+        self._check(self.lib.hbx_broadcast_decode_d(
+            self.h, d_shards.data_ptr(), d_present.data_ptr(), d_root.data_ptr(), inst, k, m, L, d_out.data_ptr(),
+            d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), stream))
 
     def get_ct_valid_d(self, d_ct_valid, stream=None):
         self._check(self.lib.hbx_get_ct_valid_d(self.h, d_ct_valid.data_ptr(), stream))

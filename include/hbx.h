@@ -40,6 +40,9 @@ extern "C" {
 #define HBX_E_NO_CIPHERTEXTS (-6)    /* hbx_prepare_ciphertexts not called / wrong p */
 #define HBX_E_INVALID_CIPHERTEXT (-7)/* Ciphertext::verify failed or undecodable (honey_badger.rs:366-373) */
 #define HBX_E_OUT_OF_MEMORY (-8)
+#define HBX_E_TOO_FEW_SHARDS (-9)    /* reed_solomon_erasure Error::TooFewShardsPresent */
+#define HBX_E_ROOT_MISMATCH (-10)    /* decode_from_shards: rebuilt Merkle root != hash (broadcast.rs:686) */
+#define HBX_E_NO_PAYLOAD (-11)       /* glue_shards: fewer than 4 bytes (broadcast.rs:702) */
 
 /* per-point decode status (hbx_set_pk_shares / hbx_prepare_ciphertexts) */
 #define HBX_PT_OK 0
@@ -137,6 +140,46 @@ int hbx_encrypt(hbx_ctx* ctx, const uint8_t* pk48, const uint8_t* msg_blob, cons
                 uint32_t p, const uint8_t* r32, uint8_t* u48, uint8_t* v_blob, uint8_t* w96);
 int hbx_decrypt_shares(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* u48, uint32_t p,
                        uint8_t* shares48);
+
+/* ---------------------------------------------------------------------------------------------
+ * Broadcast: Reed-Solomon erasure coding and the Merkle tree over shards (SURVEY.md §8 rows
+ * C1-C5d), batched over `inst` broadcast instances.  Device pointers, stream-ordered.
+ * Shards of one instance are contiguous: d_shards[inst][k + m][L]; leaf i of an instance is the
+ * index byte i followed by shard i (src/broadcast.rs:373-377).  Requires k + m <= 256, k <= 128.
+ *
+ * hbx_rs_encode_d -- ReedSolomon::encode (reed-solomon-erasure 3.1.0) via Coding::encode
+ *   (src/broadcast.rs:632-640, called at :365): fills the m parity shards of every instance.
+ * hbx_rs_reconstruct_d -- ReedSolomon::reconstruct_shards via Coding::reconstruct_shards
+ *   (src/broadcast.rs:643-657, called at :667): rebuilds every shard whose d_present byte is 0
+ *   from the first k present shards.  d_status[inst]: HBX_OK or HBX_E_TOO_FEW_SHARDS.
+ * hbx_merkle_roots_d -- MerkleTree::from_vec(&SHA256, leaves).root_hash() (src/broadcast.rs:381,
+ *   :683-686) over the index-prefixed shards: d_roots[inst][32].
+ * hbx_merkle_validate_d -- Broadcast::validate_proof (src/broadcast.rs:555-575):
+ *   Proof::validate(&root_hash) && node_index(sender) == value[0] && Proof::index(count) == value[0],
+ *   for nproofs flattened proofs: d_values[j][vlen] (the leaf: index byte + shard),
+ *   d_node_hash[j][17][32] (lemma node hashes from the root down to the leaf hash),
+ *   d_sib_hash[j][16][32], d_sides[j] (bit l: the level-l sibling is Positioned::Left),
+ *   d_depth[j], d_root[j][32] (the proof's root_hash), d_sender[j]; d_valid[j] out.
+ * hbx_broadcast_decode_d -- decode_from_shards + glue_shards (src/broadcast.rs:660-707):
+ *   reconstruct, rebuild the tree, compare with d_root_expect[inst][32], glue the first k shards.
+ *   d_out[inst][out_stride], d_out_len[inst], d_status[inst]: HBX_OK / HBX_E_TOO_FEW_SHARDS /
+ *   HBX_E_ROOT_MISMATCH / HBX_E_NO_PAYLOAD.  With m == 0 (Coding::Trivial) any absent shard
+ *   is HBX_E_TOO_FEW_SHARDS.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_rs_encode_d(hbx_ctx* ctx, uint8_t* d_shards, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                    void* stream);
+int hbx_rs_reconstruct_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t* d_present, uint32_t inst, uint32_t k,
+                         uint32_t m, uint32_t L, int32_t* d_status, void* stream);
+int hbx_merkle_roots_d(hbx_ctx* ctx, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L,
+                       uint8_t* d_roots, void* stream);
+int hbx_merkle_validate_d(hbx_ctx* ctx, const uint8_t* d_values, uint32_t vlen, const uint8_t* d_node_hash,
+                          const uint8_t* d_sib_hash, const uint32_t* d_sides, const uint32_t* d_depth,
+                          const uint8_t* d_root, const uint32_t* d_sender, uint32_t count, uint32_t nproofs,
+                          uint8_t* d_valid, void* stream);
+int hbx_broadcast_decode_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t* d_present,
+                           const uint8_t* d_root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                           uint8_t* d_out, uint64_t out_stride, uint64_t* d_out_len, int32_t* d_status,
+                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,176 @@
+"""GPU parity for the Broadcast byte path against the
+oracle (oracle/rs_merkle.py): RS parity bytes, reconstructed shards, Merkle roots, proof-validation
+bits and decoded values must be identical.  Cases follow the reference's tests/broadcast.rs
+(sizes 1..5 and larger, payloads b"Foo" and 32 spaces, f silent nodes) plus erasure patterns with
+too few shards, corrupted proofs and a wrong root."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import rs_merkle as rm
+
+torch = pytest.importorskip("torch")
+
+HBX_E_TOO_FEW_SHARDS = -9
+HBX_E_ROOT_MISMATCH = -10
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,L,inst", [(2, 2, 5, 3), (3, 4, 37, 2), (5, 8, 64, 4), (44, 84, 1000, 2), (86, 170, 33, 1)])
+def test_rs_encode(hbx_ctx, k, m, L, inst):
+    rng = np.random.default_rng(k * 1000 + L)
+    data = np.zeros((inst, k + m, L), dtype=np.uint8)
+    data[:, :k] = rng.integers(0, 256, size=(inst, k, L), dtype=np.uint8)
+    d = dev(data)
+    hbx_ctx.rs_encode_d(d, k, m)
+    torch.cuda.synchronize()
+    rs = rm.ReedSolomon(k, m)
+    out = d.cpu().numpy()
+    for i in range(inst):
+        np.testing.assert_array_equal(out[i], rs.encode(data[i]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,L", [(2, 2, 9), (3, 4, 37), (44, 84, 257)])
+def test_rs_reconstruct(hbx_ctx, k, m, L):
+    n = k + m
+    rs = rm.ReedSolomon(k, m)
+    rng = np.random.default_rng(n + L)
+    inst = 6
+    full = np.zeros((inst, n, L), dtype=np.uint8)
+    present = np.ones((inst, n), dtype=np.uint8)
+    for i in range(inst):
+        buf = np.zeros((n, L), dtype=np.uint8)
+        buf[:k] = rng.integers(0, 256, size=(k, L), dtype=np.uint8)
+        full[i] = rs.encode(buf)
+        r = random.Random(i)
+        nmiss = [0, m, m // 2, 1, m + 1, n][i]            # all present / max erasures / ... / too few
+        for j in r.sample(range(n), min(nmiss, n)):
+            present[i, j] = 0
+    damaged = full.copy()
+    damaged[present == 0] = 0xA5
+    d = dev(damaged)
+    st = torch.zeros(inst, dtype=torch.int32, device="cuda")
+    hbx_ctx.rs_reconstruct_d(d, dev(present), st, k, m)
+    torch.cuda.synchronize()
+    out, st = d.cpu().numpy(), st.cpu().numpy()
+    for i in range(inst):
+        shards = [full[i, j].tobytes() if present[i, j] else None for j in range(n)]
+        try:
+            want = rs.reconstruct(shards)
+        except rm.TooFewShardsPresent:
+            assert st[i] == HBX_E_TOO_FEW_SHARDS
+            continue
+        assert st[i] == 0
+        assert [out[i, j].tobytes() for j in range(n)] == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L", [(1, 3), (2, 7), (3, 1), (4, 5), (7, 64), (10, 65), (128, 300), (256, 4)])
+def test_merkle_roots(hbx_ctx, n, L):
+    rng = np.random.default_rng(n * 7 + L)
+    inst = 3
+    shards = rng.integers(0, 256, size=(inst, n, L), dtype=np.uint8)
+    roots = torch.zeros((inst, 32), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_roots_d(dev(shards), roots)
+    torch.cuda.synchronize()
+    for i in range(inst):
+        leaves = [bytes([j & 0xFF]) + shards[i, j].tobytes() for j in range(n)]
+        assert roots[i].cpu().numpy().tobytes() == rm.MerkleTree(leaves).root_hash()
+
+
+def flatten(proofs, senders):
+    P = len(proofs)
+    vlen = len(proofs[0]["value"])
+    vals = np.zeros((P, vlen), dtype=np.uint8)
+    nodes = np.zeros((P, 17, 32), dtype=np.uint8)
+    sibs = np.zeros((P, 16, 32), dtype=np.uint8)
+    sides = np.zeros(P, dtype=np.uint32)
+    depth = np.zeros(P, dtype=np.uint32)
+    roots = np.zeros((P, 32), dtype=np.uint8)
+    for j, p in enumerate(proofs):
+        vals[j] = np.frombuffer(p["value"], dtype=np.uint8)
+        lem = p["lemma"]
+        depth[j] = len(lem) - 1
+        for lv, (h, sib) in enumerate(lem):
+            nodes[j, lv] = np.frombuffer(h, dtype=np.uint8)
+            if sib is not None:
+                sibs[j, lv] = np.frombuffer(sib[1], dtype=np.uint8)
+                if sib[0] == "L":
+                    sides[j] |= 1 << lv
+        roots[j] = np.frombuffer(p["root_hash"], dtype=np.uint8)
+    return vals, nodes, sibs, sides, depth, roots, np.asarray(senders, dtype=np.uint32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 7, 13, 128])
+def test_merkle_validate(hbx_ctx, n):
+    value = bytes(range(256)) * 3
+    _, leaves, tree = rm.send_shards(value, n)
+    proofs, senders = [], []
+    for i, leaf in enumerate(leaves):
+        p = tree.gen_proof(leaf)
+        proofs.append(p)
+        senders.append(i)
+        if i % 3 == 0:                       # wrong sender (node_index check)
+            proofs.append(p)
+            senders.append((i + 1) % n)
+        if i % 4 == 1:                       # corrupted value byte
+            proofs.append(dict(p, value=p["value"][:-1] + bytes([p["value"][-1] ^ 1])))
+            senders.append(i)
+        if i % 5 == 2 and len(p["lemma"]) > 1:  # corrupted sibling hash
+            lem = list(p["lemma"])
+            h, (side, sh) = lem[0]
+            lem[0] = (h, (side, bytes([sh[0] ^ 0x80]) + sh[1:]))
+            proofs.append(dict(p, lemma=lem))
+            senders.append(i)
+        if i % 7 == 3:                       # proof for another root
+            proofs.append(dict(p, root_hash=b"\x11" * 32))
+            senders.append(i)
+    arrs = flatten(proofs, senders)
+    valid = torch.zeros(len(proofs), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_validate_d(*[dev(a) for a in arrs], n, valid)
+    torch.cuda.synchronize()
+    want = [rm.validate_broadcast_proof(p, s, n) for p, s in zip(proofs, senders)]
+    assert valid.cpu().numpy().astype(bool).tolist() == want
+    assert sum(want) == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 8, 13, 40, 128])
+@pytest.mark.parametrize("value", [b"Foo", b" " * 32, bytes(range(256)) * 5])
+def test_broadcast_decode(hbx_ctx, n, value):
+    f = rm.num_faulty(n)
+    k, m = rm.coding_counts(n)
+    shards, leaves, tree = rm.send_shards(value, n)
+    L = shards.shape[1]
+    inst = 3   # 0: f silent (the last f), 1: wrong root, 2: one too many missing (when m > 0)
+    buf = np.stack([shards] * inst)
+    present = np.ones((inst, n), dtype=np.uint8)
+    present[0, n - f:] = 0
+    present[1, : f] = 0
+    if m > 0:
+        present[2, : m + 1] = 0
+    buf[present == 0] = 0
+    roots = np.stack([np.frombuffer(tree.root_hash(), dtype=np.uint8)] * inst).copy()
+    roots[1, 0] ^= 1
+    out = torch.zeros((inst, k * L), dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(inst, dtype=torch.int64, device="cuda")
+    st = torch.zeros(inst, dtype=torch.int32, device="cuda")
+    hbx_ctx.broadcast_decode_d(dev(buf), dev(present), dev(roots), k, m, out, out_len, st)
+    torch.cuda.synchronize()
+    st, out_len, out = st.cpu().numpy(), out_len.cpu().numpy(), out.cpu().numpy()
+    for i in range(inst):
+        vals = [leaves[j] if present[i, j] else None for j in range(n)]
+        want = rm.decode_from_shards(vals, n, roots[i].tobytes())
+        if want is None:
+            assert st[i] in (HBX_E_TOO_FEW_SHARDS, HBX_E_ROOT_MISMATCH), (i, st[i])
+        else:
+            assert st[i] == 0, (i, st[i])
+            assert out[i, : out_len[i]].tobytes() == want
+    assert st[0] == 0 and out[0, : out_len[0]].tobytes() == value
