@@ -69,6 +69,10 @@ struct hbx_ctx {
   dbuf gf_log, gf_exp;
   uint32_t rs_k = 0, rs_m = 0;
   dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, roots;
+  // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
+  uint32_t coin_I = 0, coin_n = 0;
+  dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
+      coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
 };
 
 static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
@@ -94,6 +98,8 @@ static void pack_bits(const uint8_t* bytes, size_t n, uint8_t* bits) {
   for (size_t k = 0; k < n; k++)
     if (bytes[k]) bits[k >> 3] |= (uint8_t)(1u << (k & 7));
 }
+
+static bool scalars_canonical(const uint8_t* s32, size_t count);
 
 // Pairing checks of jobs [q_first, q_last] of every proposer (q < n: shares, q == n: ciphertext).
 static int launch_pair_checks(hbx_ctx* c, hipStream_t s, uint32_t n, uint32_t p, uint32_t q_first, uint32_t q_last,
@@ -278,7 +284,11 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->S_status, &c->fallback,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
                   &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef,
-                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots};
+                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots,
+                  &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
+                  &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
+                  &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
+                  &c->coin_out96};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -494,6 +504,131 @@ int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_prese
   hipLaunchKernelGGL(k_glue, dim3(inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, k, L, d_out,
                      (size_t)out_stride, d_out_len, d_status);
   HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+// ---- Common Coin ----------------------------------------------------------------------------
+int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* nonce_off, uint32_t count,
+                       uint8_t* h96) {
+  if (!c || !nonce_off || count == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_nonces: bad args");
+  for (uint32_t j = 0; j < count; j++)
+    if (nonce_off[j + 1] < nonce_off[j]) return fail(c, HBX_E_INVALID_ARG, "nonce_off not monotone");
+  const uint64_t total = nonce_off[count];
+  if (total && !nonce_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_nonces: null blob");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (!c->coin_blob.ensure(total ? total : 16) || !c->coin_off.ensure((size_t)(count + 1) * 8) ||
+      !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
+      !c->coin_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->coin_out96.ensure((size_t)count * 96))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
+  if (total) HIPCHK(c, hipMemcpyAsync(c->coin_blob.p, nonce_blob, total, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->coin_off.p, nonce_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_hash_nonces, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
+                     c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_prepare_lines, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+                     c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>());
+  HIPCHK(c, hipGetLastError());
+  if (h96) {
+    hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+                       c->coin_out96.as<uint8_t>());
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h96, c->coin_out96.p, (size_t)count * 96, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(c, hipStreamSynchronize(s));
+  c->coin_I = count;
+  return HBX_OK;
+}
+
+int hbx_sign(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* sig96) {
+  if (!c || !sk32 || !sig96 || n == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_sign: bad args");
+  if (c->coin_I == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "hbx_prepare_nonces has not been called");
+  if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_sign: scalar >= r");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t m = (size_t)n * c->coin_I;
+  if (!c->coin_sk.ensure((size_t)n * 32) || !c->coin_sig96.ensure(m * 96))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_sign: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->coin_sk.p, sk32, (size_t)n * 32, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_sign, dim3((n + 63) / 64, c->coin_I), dim3(64), 0, s, c->coin_sk.as<uint8_t>(), n,
+                     c->coin_H.as<g2a>(), c->coin_sig96.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(sig96, c->coin_sig96.p, m * 96, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return HBX_OK;
+}
+
+int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* present_bits, uint32_t n, uint32_t count,
+                          uint8_t* valid_bits) {
+  if (!c || !sig96 || n == 0 || count == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sig_shares: bad args");
+  if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
+  if (count != c->coin_I) return fail(c, HBX_E_NO_CIPHERTEXTS, "%u instances but %u nonces prepared", count, c->coin_I);
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t m = (size_t)n * count;
+  if (!c->coin_sig96.ensure(m * 96) || !c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) ||
+      !c->coin_valid.ensure(m) || (present_bits && !c->coin_present.ensure(m)))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->coin_sig96.p, sig96, m * 96, hipMemcpyHostToDevice, s));
+  std::vector<uint8_t> pres;
+  if (present_bits) {
+    pres.resize(m);
+    for (size_t k = 0; k < m; k++) pres[k] = (present_bits[k >> 3] >> (k & 7)) & 1;
+    HIPCHK(c, hipMemcpyAsync(c->coin_present.p, pres.data(), m, hipMemcpyHostToDevice, s));
+  }
+  hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, c->coin_sig96.as<uint8_t>(), m,
+                     c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
+                     c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
+                     c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
+                     c->coin_valid.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  std::vector<uint8_t> v(m);
+  HIPCHK(c, hipMemcpyAsync(v.data(), c->coin_valid.p, m, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (valid_bits) pack_bits(v.data(), m, valid_bits);
+  c->coin_n = n;
+  return HBX_OK;
+}
+
+int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96, int32_t* status,
+                           uint8_t* master_ok_bits, uint8_t* parity_bits) {
+  if (!c || !master_pk48 || t == 0 || t > (uint32_t)COMBINE_MAX_T)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_combine_signatures: bad args");
+  if (c->coin_n == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified signature shares");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const uint32_t I = c->coin_I;
+  if (!c->coin_comb.ensure((size_t)I * sizeof(g2a)) || !c->coin_comb_st.ensure((size_t)I * 4) ||
+      !c->coin_mpk_comp.ensure(48) || !c->coin_mpk.ensure(sizeof(g1a)) || !c->coin_mpk_st.ensure(4) ||
+      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_signatures: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, s, c->coin_mpk_comp.as<uint8_t>(), 1u, c->coin_mpk.as<g1a>(),
+                     c->coin_mpk_st.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  int32_t mst = 0;
+  HIPCHK(c, hipMemcpyAsync(&mst, c->coin_mpk_st.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
+  hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
+                     c->coin_sig.as<g2a>(), c->coin_n, t, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_master_verify, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
+                     c->coin_H.as<g2a>(), c->coin_mpk.as<g1a>(), c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(),
+                     I, c->coin_ok.as<uint8_t>(), c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  std::vector<uint8_t> ok(I), par(I);
+  std::vector<int32_t> st(I);
+  if (sig96) HIPCHK(c, hipMemcpyAsync(sig96, c->coin_out96.p, (size_t)I * 96, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(ok.data(), c->coin_ok.p, I, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(par.data(), c->coin_par.p, I, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(st.data(), c->coin_comb_st.p, (size_t)I * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (status) memcpy(status, st.data(), (size_t)I * 4);
+  if (master_ok_bits) pack_bits(ok.data(), I, master_ok_bits);
+  if (parity_bits) pack_bits(par.data(), I, parity_bits);
   return HBX_OK;
 }
 

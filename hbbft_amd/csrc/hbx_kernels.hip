@@ -116,6 +116,26 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   valid[idx] = v ? 1 : 0;
 }
 
+// threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
+// x = index + 1 (canonical, little-endian limbs out).
+__device__ fr lagrange_at_zero(const uint16_t* idx, int t, int k) {
+  fr num = fr_from_const(FR_ONE), den = fr_from_const(FR_ONE);
+  fr xk;
+  for (int q = 0; q < 8; q++) xk.l[q] = 0;
+  xk.l[0] = (uint32_t)idx[k] + 1;
+  xk = fr_to_mont(xk);
+  for (int m = 0; m < t; m++) {
+    if (m == k) continue;
+    fr xm;
+    for (int q = 0; q < 8; q++) xm.l[q] = 0;
+    xm.l[0] = (uint32_t)idx[m] + 1;
+    xm = fr_to_mont(xm);
+    num = fr_mul(num, xm);
+    den = fr_mul(den, fr_sub(xm, xk));
+  }
+  return fr_from_mont(fr_mul(num, fr_inv(den)));
+}
+
 // Lagrange combine of the first t valid shares of proposer j (one 256-thread block per
 // proposer), then the hash_bytes key = SHA-256(compress(g)).
 constexpr int COMBINE_THREADS = 256;
@@ -145,22 +165,7 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   }
   g1j acc = g1_identity();
   for (int k = tid; k < (int)t; k += COMBINE_THREADS) {
-    // lambda_k(0) = prod_{m != k} x_m / (x_m - x_k), x = index + 1
-    fr num = fr_from_const(FR_ONE), den = fr_from_const(FR_ONE);
-    fr xk;
-    for (int q = 0; q < 8; q++) xk.l[q] = 0;
-    xk.l[0] = (uint32_t)idx[k] + 1;
-    xk = fr_to_mont(xk);
-    for (int m = 0; m < (int)t; m++) {
-      if (m == k) continue;
-      fr xm;
-      for (int q = 0; q < 8; q++) xm.l[q] = 0;
-      xm.l[0] = (uint32_t)idx[m] + 1;
-      xm = fr_to_mont(xm);
-      num = fr_mul(num, xm);
-      den = fr_mul(den, fr_sub(xm, xk));
-    }
-    const fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
+    const fr lam = lagrange_at_zero(idx, (int)t, k);
     const g1a sp = S[(size_t)j * n + idx[k]];
     const g1j part = g1_mul_scalar(g1_from_affine(sp), lam.l);
     acc = g1_add(acc, part);
@@ -434,6 +439,152 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (size_t)n * p) return;
   if (!ct_valid[k / n]) valid[k] = 0;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Common Coin (reference src/common_coin.rs)
+// ----------------------------------------------------------------------------------------------
+// H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one lane each.
+__global__ void __launch_bounds__(64) k_hash_nonces(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                    uint32_t count, g2a* __restrict__ H) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  uint8_t d[32];
+  sha256_2(blob + off[j], off[j + 1] - off[j], nullptr, 0, d);
+  H[j] = g2_to_affine(hash_g2_from_digest(d));
+}
+
+__global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict__ comp, size_t count,
+                                                      g2a* __restrict__ out, int32_t* __restrict__ status) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  g2a p;
+  status[i] = g2_decompress(comp + i * 96, p);
+  out[i] = p;
+}
+
+// e(PA, QA) e(PB, QB) == 1 with QA prepared and QB's lines on the fly; pairings with the
+// identity contribute 1.
+__device__ __forceinline__ bool check_mixed(const line_pre* LA, const g1a& PA, bool qa_inf, const g2a& QB,
+                                            const g1a& PB) {
+  const bool skipA = PA.inf || qa_inf;
+  const bool skipB = PB.inf || QB.inf;
+  if (skipA && skipB) return true;
+  const fq12 f = skipB ? miller_loop2(LA, PA, true, LA, PA, false) : miller_loop_mixed(LA, PA, !skipA, QB, PB, true);
+  return fq12_is_one(final_exponentiation(f));
+}
+
+// B1: PublicKeyShare::verify(share, nonce) (common_coin.rs:151): e(pk_i, H) == e(g1, sig_i),
+// i.e. e(pk_i, H) e(-g1, sig_i) == 1.  Lane = node i, blockIdx.y = coin instance.
+__global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __restrict__ lines, const g2a* __restrict__ H,
+                                                          const g1a* __restrict__ pk, uint32_t n_keys,
+                                                          const g2a* __restrict__ sig,
+                                                          const int32_t* __restrict__ sig_status,
+                                                          const uint8_t* __restrict__ present, uint32_t n,
+                                                          uint8_t* __restrict__ valid) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t inst = blockIdx.y;
+  if (i >= n) return;
+  const size_t idx = (size_t)inst * n + i;
+  const int32_t st = sig_status[idx];
+  bool v = false;
+  if ((st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && (present == nullptr || present[idx])) {
+    g1a ng;
+    ng.x = fq_from_const(G1_GEN_X);
+    ng.y = fq_neg(fq_from_const(G1_GEN_Y));
+    ng.inf = false;
+    v = check_mixed(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng);
+  }
+  valid[idx] = v ? 1 : 0;
+}
+
+// B3: PublicKeySet::combine_signatures over the first t valid shares in node-index order
+// (common_coin.rs:190; received_shares is a BTreeMap): Lagrange at 0 in G2, one 128-thread block
+// per instance.  status: 0 or HBX_E_NOT_ENOUGH_SHARDS-style -3 (NotEnoughShares).
+constexpr int SIGCOMB_THREADS = 128;
+__global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t* __restrict__ valid,
+                                                                  const g2a* __restrict__ sig, uint32_t n, uint32_t t,
+                                                                  g2a* __restrict__ out, int32_t* __restrict__ status) {
+  __shared__ uint16_t idx[COMBINE_MAX_T];
+  __shared__ int s_count;
+  __shared__ g2j red[SIGCOMB_THREADS];
+  const uint32_t inst = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int c = 0;
+    for (uint32_t i = 0; i < n && c < (int)t; i++)
+      if (valid[(size_t)inst * n + i]) idx[c++] = (uint16_t)i;
+    s_count = c;
+  }
+  __syncthreads();
+  if (s_count < (int)t) {
+    if (tid == 0) {
+      status[inst] = -3;
+      out[inst].inf = true;
+    }
+    return;
+  }
+  g2j acc = g2_identity();
+  for (int k = tid; k < (int)t; k += SIGCOMB_THREADS) {
+    const fr lam = lagrange_at_zero(idx, (int)t, k);
+    acc = g2_add(acc, g2_mul_bits(g2_from_affine(sig[(size_t)inst * n + idx[k]]), lam.l, 256));
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int stride = SIGCOMB_THREADS / 2; stride > 0; stride >>= 1) {
+    if (tid < stride) red[tid] = g2_add(red[tid], red[tid + stride]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out[inst] = g2_to_affine(red[0]);
+    status[inst] = 0;
+  }
+}
+
+// B3 master check (PublicKey::verify, common_coin.rs:196) + B4 Signature::parity (:173) +
+// the compressed signature, one lane per instance.
+__global__ void __launch_bounds__(64) k_master_verify(const line_pre* __restrict__ lines, const g2a* __restrict__ H,
+                                                      const g1a* __restrict__ master_pk, const g2a* __restrict__ sig,
+                                                      const int32_t* __restrict__ status, uint32_t count,
+                                                      uint8_t* __restrict__ master_ok, uint8_t* __restrict__ parity,
+                                                      uint8_t* __restrict__ sig96) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  if (status[j] != 0) {
+    master_ok[j] = 0;
+    parity[j] = 0;
+    for (int q = 0; q < 96; q++) sig96[(size_t)j * 96 + q] = 0;
+    return;
+  }
+  g1a ng;
+  ng.x = fq_from_const(G1_GEN_X);
+  ng.y = fq_neg(fq_from_const(G1_GEN_Y));
+  ng.inf = false;
+  const g2a s = sig[j];
+  master_ok[j] = check_mixed(lines + (size_t)j * MILLER_LINES, master_pk[0], H[j].inf, s, ng) ? 1 : 0;
+  uint8_t u[192];
+  g2_uncompressed(s, u);
+  uint8_t x = 0;
+  for (int q = 0; q < 192; q++) x ^= u[q];
+  parity[j] = (uint8_t)(__builtin_popcount(x) & 1);
+  g2_compress(s, sig96 + (size_t)j * 96);
+}
+
+__global__ void __launch_bounds__(64) k_compress_g2(const g2a* __restrict__ pts, uint32_t count,
+                                                    uint8_t* __restrict__ out96) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < count) g2_compress(pts[j], out96 + (size_t)j * 96);
+}
+
+// SecretKeyShare::sign (common_coin.rs:142): sig[inst][i] = sk_i * H_inst, compressed.
+__global__ void __launch_bounds__(64) k_sign(const uint8_t* __restrict__ sk32, uint32_t n, const g2a* __restrict__ H,
+                                             uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t inst = blockIdx.y;
+  if (i >= n) return;
+  uint32_t k[8];
+  fr_from_be32(sk32 + (size_t)i * 32, k);
+  g2_compress(g2_to_affine(g2_mul_bits(g2_from_affine(H[inst]), k, 256)), out96 + ((size_t)inst * n + i) * 96);
 }
 
 }  // namespace hbx

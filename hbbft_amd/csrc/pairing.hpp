@@ -132,6 +132,49 @@ HBX_HDNI fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const l
   return fq12_conj(f);
 }
 
+// f * (c0 + c1 v + c4 v w) with c4 in Fq2: an UN-normalised line (l scaled by its Fq2 factor,
+// which the final exponentiation removes) evaluated at a G1 point.
+HBX_HDNI fq12 fq12_mul_by_014_f2(const fq12& f, const fq2& c0, const fq2& c1, const fq2& c4) {
+  const fq6 aa = fq6_mul_by_01(f.c0, c0, c1);
+  const fq6 bb = fq6{fq2_mul_xi(fq2_mul(f.c1.c2, c4)), fq2_mul(f.c1.c0, c4), fq2_mul(f.c1.c1, c4)};
+  const fq2 o = fq2_add(c1, c4);
+  fq6 s = fq6_add(f.c1, f.c0);
+  s = fq6_mul_by_01(s, c0, o);
+  const fq6 n1 = fq6_sub(fq6_sub(s, aa), bb);
+  const fq6 n0 = fq6_add(fq6_mul_v(bb), aa);
+  return fq12{n0, n1};
+}
+
+// Two-pair Miller loop where pair A uses prepared lines and pair B's G2 point varies per check
+// (a signature share, common_coin.rs:151): B's lines are generated on the fly from T = QB and
+// evaluated un-normalised at PB.  Returns conj(f) like miller_loop2.
+HBX_HDNI fq12 miller_loop_mixed(const line_pre* LA, const g1a& PA, bool useA, const g2a& QB, const g1a& PB,
+                                bool useB) {
+  fq12 f = fq12_one();
+  g2j T = g2_from_affine(QB);
+  int k = 0;
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12_sqr(f);
+    if (useA) f = mul_by_line(f, LA[k], PA);
+    if (useB) {
+      fq2 c0, c1, c2;
+      line_dbl_step(T, c0, c1, c2);
+      f = fq12_mul_by_014_f2(f, c0, fq2_mul_fq(c1, PB.x), fq2_mul_fq(c2, PB.y));
+    }
+    k++;
+    if ((BLS_X >> i) & 1) {
+      if (useA) f = mul_by_line(f, LA[k], PA);
+      if (useB) {
+        fq2 c0, c1, c2;
+        line_add_step(T, QB, c0, c1, c2);
+        f = fq12_mul_by_014_f2(f, c0, fq2_mul_fq(c1, PB.x), fq2_mul_fq(c2, PB.y));
+      }
+      k++;
+    }
+  }
+  return fq12_conj(f);
+}
+
 // g^|x| for g in the cyclotomic subgroup.
 HBX_HDNI fq12 cyc_exp_abs_x(const fq12& g) {
   fq12 r = g;

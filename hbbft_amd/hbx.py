@@ -45,6 +45,10 @@ EXPORTS = (
     "hbx_public_keys",
     "hbx_encrypt",
     "hbx_decrypt_shares",
+    "hbx_prepare_nonces",
+    "hbx_sign",
+    "hbx_verify_sig_shares",
+    "hbx_combine_signatures",
     "hbx_rs_encode_d",
     "hbx_rs_reconstruct_d",
     "hbx_merkle_roots_d",
@@ -87,6 +91,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
     lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
     lib.hbx_get_ct_valid_d.argtypes = [P, P, P]
+    lib.hbx_prepare_nonces.argtypes = [P, u8p, u64p, u32, u8p]
+    lib.hbx_sign.argtypes = [P, u8p, u32, u8p]
+    lib.hbx_verify_sig_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
+    lib.hbx_combine_signatures.argtypes = [P, u8p, u32, u8p, i32p, u8p, u8p]
     lib.hbx_rs_encode_d.argtypes = [P, P, u32, u32, u32, u32, P]
     lib.hbx_rs_reconstruct_d.argtypes = [P, P, P, u32, u32, u32, u32, P, P]
     lib.hbx_merkle_roots_d.argtypes = [P, P, u32, u32, u32, P, P]
@@ -232,6 +240,49 @@ class Context:
         self._check(self.lib.hbx_verify_dec_shares_d(
             self.h, d_shares.data_ptr(), None if d_present is None else d_present.data_ptr(), n, p,
             None if d_valid is None else d_valid.data_ptr(), stream))
+
+    # -- common coin ------------------------------------------------------------------------------
+    def prepare_nonces(self, nonces: Sequence[bytes]) -> np.ndarray:
+        """hash_g2 of every nonce (+ prepared lines); returns uint8[count, 96] compressed points."""
+        count = len(nonces)
+        off = np.zeros(count + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(x) for x in nonces])
+        blob = np.frombuffer(b"".join(nonces) or b"\0", dtype=np.uint8).copy()
+        h = np.zeros((count, 96), dtype=np.uint8)
+        self._check(self.lib.hbx_prepare_nonces(self.h, _u8(blob), off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                count, _u8(h)))
+        self._coin_count = count
+        return h
+
+    def sign(self, sk32: np.ndarray) -> np.ndarray:
+        """uint8[n, 32] scalars -> uint8[count, n, 96] signature shares of the prepared nonces."""
+        sk32 = np.ascontiguousarray(sk32, dtype=np.uint8)
+        n = sk32.shape[0]
+        out = np.zeros((self._coin_count, n, 96), dtype=np.uint8)
+        self._check(self.lib.hbx_sign(self.h, _u8(sk32), n, _u8(out)))
+        return out
+
+    def verify_sig_shares(self, sigs: np.ndarray, present: Optional[np.ndarray] = None) -> np.ndarray:
+        """sigs: uint8[count, n, 96] -> bool[count, n]."""
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+        count, n, _ = sigs.shape
+        pres = None if present is None else pack_bits(np.asarray(present, dtype=bool).reshape(-1))
+        bits = np.zeros((count * n + 7) // 8, dtype=np.uint8)
+        self._check(self.lib.hbx_verify_sig_shares(self.h, _u8(sigs), None if pres is None else _u8(pres), n, count,
+                                                   _u8(bits)))
+        return unpack_bits(bits, count * n).reshape(count, n)
+
+    def combine_signatures(self, master_pk48: bytes, t: int):
+        """-> (sig uint8[count, 96], status int32[count], master_ok bool[count], parity bool[count])."""
+        count = self._coin_count
+        sig = np.zeros((count, 96), dtype=np.uint8)
+        st = np.zeros(count, dtype=np.int32)
+        ok = np.zeros((count + 7) // 8, dtype=np.uint8)
+        par = np.zeros((count + 7) // 8, dtype=np.uint8)
+        mpk = np.frombuffer(bytes(master_pk48), dtype=np.uint8).copy()
+        self._check(self.lib.hbx_combine_signatures(self.h, _u8(mpk), t, _u8(sig),
+                                                    st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _u8(ok), _u8(par)))
+        return sig, st, unpack_bits(ok, count), unpack_bits(par, count)
 
     # -- broadcast (torch tensors as HBM buffers) ------------------------------------------------
     def rs_encode_d(self, d_shards, k: int, m: int, stream=None):

@@ -142,6 +142,27 @@ int hbx_decrypt_shares(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint
                        uint8_t* shares48);
 
 /* ---------------------------------------------------------------------------------------------
+ * Common Coin, batched over `count` coin instances (concurrent
+ * Agreement instances; the nonce of each is Nonce::new, src/agreement/mod.rs:155-165).
+ * hbx_prepare_nonces -- hash_g2(nonce_i) once per instance (threshold_crypto, hoisted out of
+ *   every share verification) + its prepared Miller lines; h96 (optional) = the compressed points.
+ * hbx_sign -- SecretKeyShare::sign (src/common_coin.rs:142): sig96[inst][i] = sk_i * hash_g2(nonce).
+ * hbx_verify_sig_shares -- PublicKeyShare::verify (src/common_coin.rs:151) for a [count][n] matrix
+ *   of compressed signature shares (present_bits NULL = all present); uses hbx_set_pk_shares keys.
+ *   Bit inst*n+i = e(pk_i, H) == e(g1, sig_i); absent / undecodable / unknown sender -> 0.
+ * hbx_combine_signatures -- PublicKeySet::combine_signatures over the first t valid shares in
+ *   node-index order (src/common_coin.rs:190) + PublicKey::verify with the master key (:196) +
+ *   Signature::parity (:173).  status[inst]: HBX_OK / HBX_E_NOT_ENOUGH_SHARES.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_prepare_nonces(hbx_ctx* ctx, const uint8_t* nonce_blob, const uint64_t* nonce_off, uint32_t count,
+                       uint8_t* h96);
+int hbx_sign(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, uint8_t* sig96);
+int hbx_verify_sig_shares(hbx_ctx* ctx, const uint8_t* sig96, const uint8_t* present_bits, uint32_t n,
+                          uint32_t count, uint8_t* valid_bits);
+int hbx_combine_signatures(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96,
+                           int32_t* status, uint8_t* master_ok_bits, uint8_t* parity_bits);
+
+/* ---------------------------------------------------------------------------------------------
  * Broadcast: Reed-Solomon erasure coding and the Merkle tree over shards (SURVEY.md §8 rows
  * C1-C5d), batched over `inst` broadcast instances.  Device pointers, stream-ordered.
  * Shards of one instance are contiguous: d_shards[inst][k + m][L]; leaf i of an instance is the

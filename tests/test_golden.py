@@ -51,3 +51,18 @@ def test_fixture_against_oracle(n):
             continue
         s = bls.g1_decompress(d["shares"][j, i].tobytes())
         assert tc.verify_decryption_share(pks[i], s, (u, v, w), hash_pt=h) == bool(d["expect_valid"][j, i])
+
+
+@pytest.mark.parametrize("n", [4])
+def test_coin_fixture_against_oracle(n):
+    d = dict(np.load(os.path.join(GOLDEN, f"coin_n{n}.npz"), allow_pickle=False))
+    off = d["nonce_off"]
+    nonces = [d["nonce_blob"][int(off[j]):int(off[j + 1])].tobytes() for j in range(len(off) - 1)]
+    for j, nonce in enumerate(nonces):
+        assert nonce.startswith(b"Nonce for Honey Badger [")
+        assert bls.g2_compress(tc.hash_g2(nonce)) == d["h"][j].tobytes()
+    # combined signature of instance 0 verifies under the master key and has the stored parity
+    sig = bls.g2_decompress(d["expect_sig"][0].tobytes())
+    h0 = bls.g2_decompress(d["h"][0].tobytes())
+    assert tc.verify_sig(bls.g1_decompress(d["master_pk"].tobytes()), sig, nonces[0], hash_pt=h0)
+    assert tc.parity(sig) == bool(d["expect_parity"][0])

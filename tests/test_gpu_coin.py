@@ -1,0 +1,46 @@
+"""GPU parity for the Common Coin path against the committed oracle
+fixtures tests/golden/coin_n{4,7}.npz (tests/golden/make_coin_golden.py): hash_g2 of the nonces,
+signature-share validity, combined signature, master verification, parity, and the producer-side
+SecretKeyShare::sign.  Bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(n):
+    return dict(np.load(os.path.join(GOLDEN, f"coin_n{n}.npz"), allow_pickle=False))
+
+
+def _nonces(d):
+    off = d["nonce_off"]
+    return [d["nonce_blob"][int(off[j]):int(off[j + 1])].tobytes() for j in range(len(off) - 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 7])
+def test_coin_matches_golden(hbx_ctx, n):
+    d = _load(n)
+    assert (hbx_ctx.set_pk_shares([r.tobytes() for r in d["pk_comp"]]) == 0).all()
+    h = hbx_ctx.prepare_nonces(_nonces(d))
+    np.testing.assert_array_equal(h, d["h"])
+    valid = hbx_ctx.verify_sig_shares(d["sigs"], d["present"])
+    np.testing.assert_array_equal(valid, d["expect_valid"])
+    sig, st, ok, par = hbx_ctx.combine_signatures(d["master_pk"].tobytes(), int(d["t"]))
+    np.testing.assert_array_equal(st, d["expect_status"])
+    good = st == 0
+    np.testing.assert_array_equal(sig[good], d["expect_sig"][good])
+    np.testing.assert_array_equal(ok[good], d["expect_master_ok"][good])
+    np.testing.assert_array_equal(par[good], d["expect_parity"][good])
+    assert ok[good].all()
+
+
+@pytest.mark.gpu
+def test_sign_matches_honest_shares(hbx_ctx):
+    d = _load(4)
+    hbx_ctx.prepare_nonces(_nonces(d))
+    sigs = hbx_ctx.sign(d["sk"])
+    honest = d["expect_valid"]
+    np.testing.assert_array_equal(sigs[honest], d["sigs"][honest])

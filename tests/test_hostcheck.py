@@ -94,3 +94,16 @@ def test_g2_clear_cofactor_psi(hc):
         assert hc.hc_g2_mul_cofactor(bls.g2_compress(pt), o2) == 0
         assert o1.raw == o2.raw == bls.g2_compress(bls.g2_mul(pt, bls.H2))
         done += 1
+
+
+def test_pairing_check_mixed_lines(hc):
+    """Signature-share check shape: pair A over prepared lines, pair B's lines generated on the
+    fly (un-normalised) from a varying G2 point."""
+    a = 0xABCDEF0123
+    pa = bls.g1_compress(bls.g1_mul(bls.G1_GEN, a))
+    h = bls.g2_compress(bls.G2_GEN)
+    ng1 = bls.g1_compress(bls.g1_neg(bls.G1_GEN))
+    sig = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a))
+    assert hc.hc_pairing_check_mixed(pa, h, ng1, sig) == 1      # e(aP, Q) e(-P, aQ) == 1
+    bad = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a + 5))
+    assert hc.hc_pairing_check_mixed(pa, h, ng1, bad) == 0

@@ -38,6 +38,18 @@ int hc_pairing_check2(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, c
   g2_prepare_lines(QB, LB, scratch);
   return pairing_check2(LA, PA, LB, PB) ? 1 : 0;
 }
+// e(PA, QA) e(PB, QB) == 1 with QA prepared and QB's lines generated on the fly
+int hc_pairing_check_mixed(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK) return -1;
+  if (g1_decompress(pb, PB) != HBX_PT_OK) return -2;
+  if (g2_decompress(qa, QA) != HBX_PT_OK) return -3;
+  if (g2_decompress(qb, QB) != HBX_PT_OK) return -4;
+  static line_pre LA[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  return fq12_is_one(final_exponentiation(miller_loop_mixed(LA, PA, true, QB, PB, true))) ? 1 : 0;
+}
 int hc_g2_clear_cofactor(const uint8_t* in96, uint8_t* out96) {
   g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
   g2_compress(g2_to_affine(g2_clear_cofactor(g2_from_affine(p))), out96); return 0;
