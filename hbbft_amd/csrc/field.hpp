@@ -199,23 +199,43 @@ HBX_HD fq fq_mul(const fq& a, const fq& b) {
 
 HBX_HD fq fq_sqr(const fq& a) { return fq_mul(a, a); }
 
+// 32-bit add/sub with carry.  Device: clang's carry builtins lower to one v_addc_co_u32 /
+// v_subb_co_u32 per limb with the carry in VCC (the portable 64-bit form compiled to ~10 VALU
+// instructions per limb on gfx950: v_lshl_add_u64 + shifts + moves).
+HBX_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t co;
+  const uint32_t r = __builtin_addc(a, b, c, &co);
+  c = co;
+  return r;
+#else
+  const uint64_t v = (uint64_t)a + b + c;
+  c = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+#endif
+}
+HBX_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t& br) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t bo;
+  const uint32_t r = __builtin_subc(a, b, br, &bo);
+  br = bo;
+  return r;
+#else
+  const uint64_t v = (uint64_t)a - b - br;
+  br = (uint32_t)(v >> 32) & 1u;
+  return (uint32_t)v;
+#endif
+}
+
 // r = a + b reduced into [0, 2p) (inputs <= 2p).
 HBX_HD fq fq_add(const fq& a, const fq& b) {
   fq s, d;
-  uint64_t carry = 0;
+  uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)a.l[i] + b.l[i] + carry;
-    s.l[i] = (uint32_t)v;
-    carry = v >> 32;
-  }
-  uint64_t borrow = 0;
+  for (int i = 0; i < 12; i++) s.l[i] = addc32(a.l[i], b.l[i], carry);
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)s.l[i] - FQ_2P[i] - borrow;
-    d.l[i] = (uint32_t)v;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 12; i++) d.l[i] = subb32(s.l[i], FQ_2P[i], borrow);
   // a + b < 4p < 2^384 so no carry out; keep s if s < 2p (borrow), else d
   fq r;
 #pragma unroll
@@ -226,21 +246,13 @@ HBX_HD fq fq_add(const fq& a, const fq& b) {
 // r = a - b (+2p if negative), result in [0, 2p].
 HBX_HD fq fq_sub(const fq& a, const fq& b) {
   fq d;
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)a.l[i] - b.l[i] - borrow;
-    d.l[i] = (uint32_t)v;
-    borrow = (v >> 32) & 1;
-  }
-  const uint32_t mask = 0u - (uint32_t)borrow;
-  uint64_t carry = 0;
+  for (int i = 0; i < 12; i++) d.l[i] = subb32(a.l[i], b.l[i], borrow);
+  const uint32_t mask = 0u - borrow;
+  uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)d.l[i] + (FQ_2P[i] & mask) + carry;
-    d.l[i] = (uint32_t)v;
-    carry = v >> 32;
-  }
+  for (int i = 0; i < 12; i++) d.l[i] = addc32(d.l[i], FQ_2P[i] & mask, carry);
   return d;
 }
 
@@ -250,13 +262,9 @@ HBX_HD fq fq_dbl(const fq& a) { return fq_add(a, a); }
 // Conditional subtract of a 12-limb constant if x >= c.
 HBX_HD fq fq_csub(const fq& x, const uint32_t* c) {
   fq d;
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)x.l[i] - c[i] - borrow;
-    d.l[i] = (uint32_t)v;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 12; i++) d.l[i] = subb32(x.l[i], c[i], borrow);
   fq r;
 #pragma unroll
   for (int i = 0; i < 12; i++) r.l[i] = borrow ? x.l[i] : d.l[i];
@@ -323,12 +331,9 @@ HBX_HD bool fq_sqrt(const fq& a, fq& out) {
 HBX_HD bool fq_lex_largest(const fq& y_mont) {
   fq y = fq_from_mont(y_mont);
   // y > (p-1)/2  <=>  (p-1)/2 - y borrows
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)FQ_P_MINUS_1_HALF[i] - y.l[i] - borrow;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 12; i++) (void)subb32(FQ_P_MINUS_1_HALF[i], y.l[i], borrow);
   return borrow != 0;
 }
 
@@ -354,12 +359,9 @@ HBX_HD void fq_to_be(const fq& a, uint8_t* b) {
 }
 // true iff canonical value < p
 HBX_HD bool fq_lt_p(const fq& a) {
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t v = (uint64_t)a.l[i] - FQ_P[i] - borrow;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 12; i++) (void)subb32(a.l[i], FQ_P[i], borrow);
   return borrow != 0;
 }
 
@@ -415,34 +417,43 @@ HBX_HD bool fq2_lex_largest(const fq2& y_mont) {
   return c > 0;
 }
 
-// Fq2 square root (p = 3 mod 4), "complex method".  Returns false for a non-residue.
+// Fq2 square root (p = 3 mod 4), norm method, two fixed exponentiations:
+//   a = a0 + a1 u is a square iff N(a) = a0^2 + a1^2 is a square in Fq (-1 is a non-residue);
+//   s = sqrt(N(a)), alpha = (a0 + s)/2, e = alpha^((p-3)/4), t = alpha e = alpha^((p+1)/4),
+//   c = t e = alpha^((p-1)/2) = +-1 and 1/t = c e, so
+//     c = +1:  x0 = t,          x1 = a1 e / 2   (x0^2 = alpha)
+//     c = -1:  x0 = -a1 e / 2,  x1 = t          (x1^2 = -alpha)
+// (pairing's Fq2::sqrt returns one of the two roots; callers normalise the sign, so the choice
+// of root does not affect any output).  a1 = 0 never reaches the norm path.
+// Step 1: the residuosity test; s is reused by step 2.
+HBX_HD bool fq2_norm_sqrt(const fq2& a, fq& s) {
+  const fq n = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+  return fq_sqrt(n, s);
+}
+// Step 2 for a known square with a1 != 0.
+HBX_HDNI fq2 fq2_sqrt_from_norm(const fq2& a, const fq& s) {
+  const fq half = fq_from_const(FQ_HALF_MONT);
+  const fq alpha = fq_mul(fq_add(a.c0, s), half);
+  const fq e = fq_pow_const(alpha, FQ_P_MINUS_3_DIV_4);
+  const fq t = fq_mul(alpha, e);
+  const fq c = fq_mul(t, e);
+  const fq h = fq_mul(fq_mul(a.c1, e), half);
+  if (fq_eq(c, fq_one())) return fq2{t, h};
+  return fq2{fq_neg(h), t};
+}
+// Square root in Fq; false for a non-residue.
 HBX_HDNI bool fq2_sqrt(const fq2& a, fq2& out) {
   if (fq_is_zero(a.c1)) {
-    fq s;
-    if (fq_sqrt(a.c0, s)) {
-      out = fq2{s, fq_zero()};
-      return true;
-    }
-    if (fq_sqrt(fq_neg(a.c0), s)) {
-      out = fq2{fq_zero(), s};
-      return true;
-    }
-    return false;
+    // one exponentiation: s^2 = a0 if a0 is a square, else s^2 = -a0 and (s u)^2 = a0
+    const fq sq = fq_pow_const(a.c0, FQ_SQRT_EXP);
+    if (fq_eq(fq_sqr(sq), a.c0)) out = fq2{sq, fq_zero()};
+    else out = fq2{fq_zero(), sq};
+    return true;
   }
-  fq alpha;
-  if (!fq_sqrt(fq_add(fq_sqr(a.c0), fq_sqr(a.c1)), alpha)) return false;
-  // inverse of 2 in Montgomery form: (p+1)/2 * R
-  fq two = fq_dbl(fq_one());
-  fq inv2 = fq_inv(two);
-  fq delta = fq_mul(fq_add(a.c0, alpha), inv2);
-  fq x0;
-  if (!fq_sqrt(delta, x0)) {
-    delta = fq_mul(fq_sub(a.c0, alpha), inv2);
-    if (!fq_sqrt(delta, x0)) return false;
-  }
-  fq x1 = fq_mul(a.c1, fq_inv(fq_dbl(x0)));
-  out = fq2{x0, x1};
-  return fq2_eq(fq2_sqr(out), a);
+  fq s;
+  if (!fq2_norm_sqrt(a, s)) return false;
+  out = fq2_sqrt_from_norm(a, s);
+  return true;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -634,13 +645,9 @@ HBX_HD fr fr_from_const(const uint32_t* c) {
 }
 HBX_HD fr fr_csub(const fr& x) {
   fr d;
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t v = (uint64_t)x.l[i] - FR_R[i] - borrow;
-    d.l[i] = (uint32_t)v;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 8; i++) d.l[i] = subb32(x.l[i], FR_R[i], borrow);
   fr r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.l[i] = borrow ? x.l[i] : d.l[i];
@@ -678,43 +685,29 @@ HBX_HDNI fr fr_mul(const fr& a, const fr& b) {
   for (int j = 0; j < 8; j++) r.l[j] = t[j];
   // t < 2r; t[8] may hold the top carry
   if (t[8]) {
-    uint64_t borrow = 0;
+    uint32_t borrow = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint64_t v = (uint64_t)r.l[i] - FR_R[i] - borrow;
-      r.l[i] = (uint32_t)v;
-      borrow = (v >> 32) & 1;
-    }
+    for (int i = 0; i < 8; i++) r.l[i] = subb32(r.l[i], FR_R[i], borrow);
     return r;
   }
   return fr_csub(r);
 }
 HBX_HD fr fr_add(const fr& a, const fr& b) {
   fr s;
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c = (uint64_t)a.l[i] + b.l[i] + (c >> 32);
-    s.l[i] = (uint32_t)c;
-  }
+  for (int i = 0; i < 8; i++) s.l[i] = addc32(a.l[i], b.l[i], c);
   return fr_csub(s);  // a + b < 2r < 2^256
 }
 HBX_HD fr fr_sub(const fr& a, const fr& b) {
   fr d;
-  uint64_t borrow = 0;
+  uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t v = (uint64_t)a.l[i] - b.l[i] - borrow;
-    d.l[i] = (uint32_t)v;
-    borrow = (v >> 32) & 1;
-  }
+  for (int i = 0; i < 8; i++) d.l[i] = subb32(a.l[i], b.l[i], borrow);
   if (borrow) {
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      c = (uint64_t)d.l[i] + FR_R[i] + (c >> 32);
-      d.l[i] = (uint32_t)c;
-    }
+    for (int i = 0; i < 8; i++) d.l[i] = addc32(d.l[i], FR_R[i], c);
   }
   return d;
 }

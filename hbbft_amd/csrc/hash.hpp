@@ -176,15 +176,31 @@ HBX_HD fq fq_rand(chacha_rng& r) {
 }
 
 // G2::rand + scale_by_cofactor (h2 * P; computed by g2_clear_cofactor, same point).
+// SIMT shape: the rejection loop only draws x and runs the residuosity test (one Fq
+// exponentiation per draw); the square root and the cofactor clearing run once, after every
+// lane of the wave has found its point, instead of once per loop trip inside the divergent loop.
 HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
   for (;;) {
-    const fq c0 = fq_rand(r);
-    const fq c1 = fq_rand(r);
-    const fq2 x = fq2{c0, c1};
-    const bool greatest = (chacha_next_u32(r) & 1u) != 0;
-    const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+    fq2 x, rhs;
+    fq s;
+    bool greatest;
+    for (;;) {
+      const fq c0 = fq_rand(r);
+      const fq c1 = fq_rand(r);
+      x = fq2{c0, c1};
+      greatest = (chacha_next_u32(r) & 1u) != 0;
+      rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+      if (fq_is_zero(rhs.c1)) {
+        // measure-zero branch (x^3 + b in Fq); handled exactly by the general square root
+        fq2 y0;
+        if (fq2_sqrt(rhs, y0)) break;
+        continue;
+      }
+      if (fq2_norm_sqrt(rhs, s)) break;
+    }
     fq2 y;
-    if (!fq2_sqrt(rhs, y)) continue;
+    if (fq_is_zero(rhs.c1)) fq2_sqrt(rhs, y);
+    else y = fq2_sqrt_from_norm(rhs, s);
     // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
     if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
     const g2j p = g2_clear_cofactor(g2j{x, y, fq2_one()});

@@ -63,13 +63,10 @@ struct acc13 {
 };
 
 __device__ __forceinline__ void acc_add(acc13& acc, const uint32_t* x) {  // acc += x (12 limbs)
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    c = (uint64_t)acc.l[i] + x[i] + (c >> 32);
-    acc.l[i] = (uint32_t)c;
-  }
-  acc.l[12] += (uint32_t)(c >> 32);
+  for (int i = 0; i < 12; i++) acc.l[i] = addc32(acc.l[i], x[i], c);
+  acc.l[12] += c;
 }
 
 // 2^k * 2p for k = 0..6 (13 limbs each) -- the reduction ladder
@@ -91,13 +88,9 @@ __device__ __forceinline__ fq acc_reduce(acc13 acc, int K) {
   for (int k = 6; k >= 0; k--) {
     if (k >= K) continue;
     uint32_t d[13];
-    uint64_t br = 0;
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 13; i++) {
-      const uint64_t v = (uint64_t)acc.l[i] - LADDER[k][i] - br;
-      d[i] = (uint32_t)v;
-      br = (v >> 32) & 1;
-    }
+    for (int i = 0; i < 13; i++) d[i] = subb32(acc.l[i], LADDER[k][i], br);
 #pragma unroll
     for (int i = 0; i < 13; i++) acc.l[i] = br ? acc.l[i] : d[i];
   }
