@@ -73,6 +73,47 @@ struct hbx_ctx {
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
       coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
+  // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
+  std::vector<hipEvent_t> ev_pool;
+};
+
+static hipEvent_t ev_get(hbx_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+static void timing_reset(hbx_ctx* c) {
+  for (auto& v : c->tev) {
+    for (auto& pr : v) {
+      c->ev_pool.push_back(pr.first);
+      c->ev_pool.push_back(pr.second);
+    }
+    v.clear();
+  }
+}
+// Records a start event before and a stop event after one kernel launch on stream s.
+struct timed {
+  hbx_ctx* c;
+  int id;
+  hipStream_t s;
+  hipEvent_t e0 = nullptr;
+  timed(hbx_ctx* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
+    if (c->timing && (e0 = ev_get(c))) (void)hipEventRecord(e0, s);
+  }
+  ~timed() {
+    if (!e0) return;
+    hipEvent_t e1 = ev_get(c);
+    if (!e1) return;
+    (void)hipEventRecord(e1, s);
+    c->tev[id].emplace_back(e0, e1);
+  }
 };
 
 static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
@@ -108,10 +149,13 @@ static int launch_pair_checks(hbx_ctx* c, hipStream_t s, uint32_t n, uint32_t p,
     return fail(c, HBX_E_OUT_OF_MEMORY, "out of device memory (fallback flags)");
   HIPCHK(c, hipMemsetAsync(c->fallback.p, 0, (size_t)p * (n + 1), s));
   const uint32_t jobs = q_last - q_first + 1;
-  hipLaunchKernelGGL(k_verify_wide, dim3((jobs + WG_GROUPS - 1) / WG_GROUPS, p), dim3(WG_THREADS), 0, s,
-                     c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
-                     c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
-                     q_first, q_last, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>(), c->fallback.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_CT_CHECKS, s);
+    hipLaunchKernelGGL(k_verify_wide, dim3((jobs + WG_GROUPS - 1) / WG_GROUPS, p), dim3(WG_THREADS), 0, s,
+                       c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
+                       c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
+                       q_first, q_last, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>(), c->fallback.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
   const size_t all = (size_t)p * (n + 1);
   hipLaunchKernelGGL(k_pair_fallback, dim3((unsigned)((all + 63) / 64)), dim3(64), 0, s, c->fallback.as<uint8_t>(),
@@ -230,11 +274,17 @@ static int rs_reconstruct(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_presen
                      c->rs_coef_d.as<uint16_t>(), c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(), d_status);
   HIPCHK(c, hipGetLastError());
   const dim3 grid((L + 1023) / 1024, inst);
-  hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_d.as<rs_job>(),
-                     c->rs_coef_d.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_RS_CODE, s);
+    hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_d.as<rs_job>(),
+                       c->rs_coef_d.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_p.as<rs_job>(),
-                     c->rs_coef_p.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_RS_CODE, s);
+    hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_p.as<rs_job>(),
+                       c->rs_coef_p.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -243,8 +293,11 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
                         hipStream_t s) {
   if (n == 0 || n > (uint32_t)RS_MAX_N) return fail(c, HBX_E_INVALID_ARG, "merkle: need 1 <= n <= 256");
   if (!c->leaf_hash.ensure((size_t)inst * n * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: leaf hashes");
-  hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                     c->leaf_hash.as<uint32_t>());
+  {
+    timed t_(c, HBX_K_MERKLE_LEAVES, s);
+    hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
+                       c->leaf_hash.as<uint32_t>());
+  }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots);
   HIPCHK(c, hipGetLastError());
@@ -278,6 +331,9 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return HBX_E_INVALID_ARG;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  timing_reset(c);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  c->ev_pool.clear();
   dbuf* bufs[] = {&c->pk,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
@@ -328,11 +384,17 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
       !c->ct_valid.ensure(p))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
   const dim3 b64(64);
-  hipLaunchKernelGGL(k_prepare_ct, dim3((p + 63) / 64), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p,
-                     c->U.as<g1a>(), c->G2pts.as<g2a>(), c->ct_ok.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_PREPARE_CT, s);
+    hipLaunchKernelGGL(k_prepare_ct, dim3((p + 63) / 64), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p,
+                       c->U.as<g1a>(), c->G2pts.as<g2a>(), c->ct_ok.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
-                     c->lines.as<line_pre>(), c->scratch.as<fq2>());
+  {
+    timed t_(c, HBX_K_PREPARE_LINES, s);
+    hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
+                       c->lines.as<line_pre>(), c->scratch.as<fq2>());
+  }
   HIPCHK(c, hipGetLastError());
   c->p_ct = p;
   c->ct_known = false;
@@ -401,9 +463,12 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     c->ct_known = true;
   }
   // share checks: throughput-bound, n*p checks -> one lane each
-  hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
-                     c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
-                     c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_VERIFY_SHARES, s);
+    hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
+                       c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
+                       c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_gate_by_ct, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, c->valid.as<uint8_t>(),
                      c->ct_valid.as<uint8_t>(), n, p);
@@ -445,9 +510,12 @@ int hbx_rs_encode_d(hbx_ctx* c, uint8_t* d_shards, uint32_t inst, uint32_t k, ui
   if (m == 0) return HBX_OK;  // Coding::Trivial
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, L, k,
-                     c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(), 0u, c->gf_log.as<uint16_t>(),
-                     c->gf_exp.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_RS_CODE, s);
+    hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, L, k,
+                       c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(), 0u, c->gf_log.as<uint16_t>(),
+                       c->gf_exp.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -523,11 +591,17 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
   if (total) HIPCHK(c, hipMemcpyAsync(c->coin_blob.p, nonce_blob, total, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->coin_off.p, nonce_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_hash_nonces, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
-                     c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>());
+  {
+    timed t_(c, HBX_K_HASH_NONCES, s);
+    hipLaunchKernelGGL(k_hash_nonces, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
+                       c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>());
+  }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_prepare_lines, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
-                     c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>());
+  {
+    timed t_(c, HBX_K_PREPARE_LINES, s);
+    hipLaunchKernelGGL(k_prepare_lines, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>());
+  }
   HIPCHK(c, hipGetLastError());
   if (h96) {
     hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
@@ -579,10 +653,13 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
   hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, c->coin_sig96.as<uint8_t>(), m,
                      c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>());
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                     c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
-                     c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
-                     c->coin_valid.as<uint8_t>());
+  {
+    timed t_(c, HBX_K_VERIFY_SIG, s);
+    hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
+                       c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
+                       c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
+                       c->coin_valid.as<uint8_t>());
+  }
   HIPCHK(c, hipGetLastError());
   std::vector<uint8_t> v(m);
   HIPCHK(c, hipMemcpyAsync(v.data(), c->coin_valid.p, m, hipMemcpyDeviceToHost, s));
@@ -612,8 +689,11 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   HIPCHK(c, hipMemcpyAsync(&mst, c->coin_mpk_st.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
-  hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
-                     c->coin_sig.as<g2a>(), c->coin_n, t, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>());
+  {
+    timed t_(c, HBX_K_COMBINE_SIGS, s);
+    hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
+                       c->coin_sig.as<g2a>(), c->coin_n, t, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>());
+  }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_master_verify, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
                      c->coin_H.as<g2a>(), c->coin_mpk.as<g1a>(), c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(),
@@ -649,8 +729,11 @@ int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* 
   const uint32_t p = c->p_ct;
   if (!c->keys.ensure((size_t)p * 32) || !c->status.ensure((size_t)p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_decrypt_d: out of device memory");
-  hipLaunchKernelGGL(k_combine, dim3(p), dim3(COMBINE_THREADS), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
-                     c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>());
+  {
+    timed t_(c, HBX_K_COMBINE, s);
+    hipLaunchKernelGGL(k_combine, dim3(p), dim3(COMBINE_THREADS), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
+                       c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>());
+  }
   HIPCHK(c, hipGetLastError());
   const uint64_t blocks = (c->max_v_len + 15) / 16;
   if (blocks) {
@@ -808,3 +891,26 @@ int hbx_decrypt_shares(hbx_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_
 }
 
 }  // extern "C"
+
+int hbx_set_timing(hbx_ctx* c, int on) {
+  if (!c) return HBX_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  timing_reset(c);
+  c->timing = on != 0;
+  return HBX_OK;
+}
+
+int hbx_kernel_time(hbx_ctx* c, int kernel, double* total_ms, uint32_t* launches) {
+  if (!c || kernel < 0 || kernel >= HBX_K_COUNT || !total_ms) return fail(c, HBX_E_INVALID_ARG, "hbx_kernel_time: bad argument");
+  HIPCHK(c, hipSetDevice(c->device));
+  double tot = 0;
+  for (auto& pr : c->tev[kernel]) {
+    HIPCHK(c, hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    tot += ms;
+  }
+  *total_ms = tot;
+  if (launches) *launches = (uint32_t)c->tev[kernel].size();
+  return HBX_OK;
+}

@@ -54,7 +54,13 @@ EXPORTS = (
     "hbx_merkle_roots_d",
     "hbx_merkle_validate_d",
     "hbx_broadcast_decode_d",
+    "hbx_set_timing",
+    "hbx_kernel_time",
 )
+
+# kernel ids of hbx_kernel_time (include/hbx.h)
+KERNELS = {"prepare_ct": 0, "prepare_lines": 1, "ct_checks": 2, "verify_shares": 3, "combine": 4,
+           "verify_sig": 5, "combine_sigs": 6, "rs_code": 7, "merkle_leaves": 8, "hash_nonces": 9}
 
 _lib = None
 
@@ -103,6 +109,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_public_keys.argtypes = [P, u8p, u32, u8p]
     lib.hbx_encrypt.argtypes = [P, u8p, u8p, u64p, u32, u8p, u8p, u8p, u8p]
     lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
+    lib.hbx_set_timing.argtypes = [P, ctypes.c_int]
+    lib.hbx_kernel_time.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
     _lib = lib
     return lib
 
@@ -152,6 +160,18 @@ class Context:
     def _check(self, rc: int):
         if rc != HBX_OK:
             raise HbxError(rc, self.lib.hbx_last_error(self.h).decode())
+
+    # -- instrumentation -----------------------------------------------------------------------
+    def set_timing(self, on: bool = True):
+        """Bracket every launch of the timed kernels with HIP events on their stream."""
+        self._check(self.lib.hbx_set_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self, name: str):
+        """(total_ms, launches) of a timed kernel since the last set_timing call."""
+        ms = ctypes.c_double()
+        cnt = ctypes.c_uint32()
+        self._check(self.lib.hbx_kernel_time(self.h, KERNELS[name], ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
 
     # -- host API ------------------------------------------------------------------------------
     def set_pk_shares(self, pk_comp: Sequence[bytes]) -> np.ndarray:

@@ -61,6 +61,24 @@ const char* hbx_last_error(const hbx_ctx* ctx);
 /* Library version string, e.g. "hbx 0.1.0 gfx950". */
 const char* hbx_version(void);
 
+/* Kernel timing (instrumentation; no reference counterpart).  With timing on, the library
+ * brackets each launch of the kernels below with HIP events recorded on the stream the kernel
+ * runs on; hbx_kernel_time synchronizes those events and reports the summed duration and the
+ * number of launches since the last hbx_set_timing call. */
+#define HBX_K_PREPARE_CT 0      /* hash_g1_g2 + decode of U/W per proposer */
+#define HBX_K_PREPARE_LINES 1   /* prepared Miller lines of H_j, W_j (and coin H) */
+#define HBX_K_CT_CHECKS 2       /* Ciphertext::verify pairing checks (wide executor) */
+#define HBX_K_VERIFY_SHARES 3   /* decryption-share pairing checks */
+#define HBX_K_COMBINE 4         /* Lagrange combine + key derivation per proposer */
+#define HBX_K_VERIFY_SIG 5      /* coin signature-share checks */
+#define HBX_K_COMBINE_SIGS 6    /* coin G2 Lagrange combine */
+#define HBX_K_RS_CODE 7         /* Reed-Solomon encode / reconstruct passes */
+#define HBX_K_MERKLE_LEAVES 8   /* SHA-256 leaf hashes */
+#define HBX_K_HASH_NONCES 9     /* coin nonce hash_g2 */
+#define HBX_K_COUNT 10
+int hbx_set_timing(hbx_ctx* ctx, int on);
+int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launches);
+
 /* ---------------------------------------------------------------------------------------------
  * Key material (once per era).
  * Replaces: NetworkInfo::new's public_key_share derivation (src/messaging.rs:251-254) and the
