@@ -472,7 +472,7 @@ HBX_HD fq6 fq6_neg(const fq6& a) { return fq6{fq2_neg(a.c0), fq2_neg(a.c1), fq2_
 HBX_HD fq6 fq6_mul_v(const fq6& a) { return fq6{fq2_mul_xi(a.c2), a.c0, a.c1}; }
 
 // Karatsuba-style Fq6 product (6 Fq2 mults).
-HBX_HDNI fq6 fq6_mul(const fq6& a, const fq6& b) {
+HBX_HD fq6 fq6_mul_i(const fq6& a, const fq6& b) {
   const fq2 t0 = fq2_mul(a.c0, b.c0);
   const fq2 t1 = fq2_mul(a.c1, b.c1);
   const fq2 t2 = fq2_mul(a.c2, b.c2);
@@ -487,8 +487,9 @@ HBX_HDNI fq6 fq6_mul(const fq6& a, const fq6& b) {
   c2 = fq2_add(fq2_sub(fq2_sub(c2, t0), t2), t1);
   return fq6{c0, c1, c2};
 }
+HBX_HDNI fq6 fq6_mul(const fq6& a, const fq6& b) { return fq6_mul_i(a, b); }
 
-HBX_HDNI fq6 fq6_sqr(const fq6& a) {
+HBX_HD fq6 fq6_sqr_i(const fq6& a) {
   // CH-SQR2
   const fq2 s0 = fq2_sqr(a.c0);
   const fq2 ab = fq2_mul(a.c0, a.c1);
@@ -502,9 +503,10 @@ HBX_HDNI fq6 fq6_sqr(const fq6& a) {
   const fq2 c2 = fq2_sub(fq2_sub(fq2_add(fq2_add(s1, s2), s3), s0), s4);
   return fq6{c0, c1, c2};
 }
+HBX_HDNI fq6 fq6_sqr(const fq6& a) { return fq6_sqr_i(a); }
 
 // a * (b0 + b1 v)   (5 Fq2 mults)
-HBX_HDNI fq6 fq6_mul_by_01(const fq6& a, const fq2& b0, const fq2& b1) {
+HBX_HD fq6 fq6_mul_by_01_i(const fq6& a, const fq2& b0, const fq2& b1) {
   const fq2 t0 = fq2_mul(a.c0, b0);
   const fq2 t1 = fq2_mul(a.c1, b1);
   // c0 = t0 + xi * (a2 * b1)
@@ -515,6 +517,7 @@ HBX_HDNI fq6 fq6_mul_by_01(const fq6& a, const fq2& b0, const fq2& b1) {
   const fq2 c2 = fq2_add(fq2_mul(a.c2, b0), t1);
   return fq6{c0, c1, c2};
 }
+HBX_HDNI fq6 fq6_mul_by_01(const fq6& a, const fq2& b0, const fq2& b1) { return fq6_mul_by_01_i(a, b0, b1); }
 
 // a * (s v) with s in Fq: (xi a2 s, a0 s, a1 s)
 HBX_HD fq6 fq6_mul_by_1_fq(const fq6& a, const fq& s) {
@@ -536,33 +539,36 @@ HBX_HDNI fq6 fq6_inv(const fq6& a) {
 HBX_HD fq12 fq12_one() { return fq12{fq6_one(), fq6_zero()}; }
 HBX_HD fq12 fq12_conj(const fq12& a) { return fq12{a.c0, fq6_neg(a.c1)}; }
 
-HBX_HDNI fq12 fq12_mul(const fq12& a, const fq12& b) {
-  const fq6 t0 = fq6_mul(a.c0, b.c0);
-  const fq6 t1 = fq6_mul(a.c1, b.c1);
-  const fq6 c1 = fq6_sub(fq6_sub(fq6_mul(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1)), t0), t1);
+HBX_HD fq12 fq12_mul_i(const fq12& a, const fq12& b) {
+  const fq6 t0 = fq6_mul_i(a.c0, b.c0);
+  const fq6 t1 = fq6_mul_i(a.c1, b.c1);
+  const fq6 c1 = fq6_sub(fq6_sub(fq6_mul_i(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1)), t0), t1);
   return fq12{fq6_add(t0, fq6_mul_v(t1)), c1};
 }
+HBX_HDNI fq12 fq12_mul(const fq12& a, const fq12& b) { return fq12_mul_i(a, b); }
 
-HBX_HDNI fq12 fq12_sqr(const fq12& a) {
+HBX_HD fq12 fq12_sqr_i(const fq12& a) {
   // complex squaring: c0 = (a0 + a1)(a0 + v a1) - ab - v ab, c1 = 2 ab
-  const fq6 ab = fq6_mul(a.c0, a.c1);
-  const fq6 t = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));
+  const fq6 ab = fq6_mul_i(a.c0, a.c1);
+  const fq6 t = fq6_mul_i(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));
   const fq6 c0 = fq6_sub(fq6_sub(t, ab), fq6_mul_v(ab));
   return fq12{c0, fq6_add(ab, ab)};
 }
+HBX_HDNI fq12 fq12_sqr(const fq12& a) { return fq12_sqr_i(a); }
 
 // f * (c0 + c1 v + c4 v w) with c0, c1 in Fq2 and c4 in Fq -- the shape of a prepared line
 // evaluated at a G1 point (pairing's mul_by_014, with c4 real).
-HBX_HDNI fq12 fq12_mul_by_014(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
-  const fq6 aa = fq6_mul_by_01(f.c0, c0, c1);
+HBX_HD fq12 fq12_mul_by_014_i(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
+  const fq6 aa = fq6_mul_by_01_i(f.c0, c0, c1);
   const fq6 bb = fq6_mul_by_1_fq(f.c1, c4);
   const fq2 o = fq2{fq_add(c1.c0, c4), c1.c1};
   fq6 s = fq6_add(f.c1, f.c0);
-  s = fq6_mul_by_01(s, c0, o);
+  s = fq6_mul_by_01_i(s, c0, o);
   const fq6 n1 = fq6_sub(fq6_sub(s, aa), bb);
   const fq6 n0 = fq6_add(fq6_mul_v(bb), aa);
   return fq12{n0, n1};
 }
+HBX_HDNI fq12 fq12_mul_by_014(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) { return fq12_mul_by_014_i(f, c0, c1, c4); }
 
 HBX_HDNI fq12 fq12_inv(const fq12& a) {
   const fq6 t = fq6_sub(fq6_sqr(a.c0), fq6_mul_v(fq6_sqr(a.c1)));
@@ -605,7 +611,7 @@ HBX_HD void fq4_sqr(const fq2& a, const fq2& b, fq2& c0, fq2& c1) {
   c0 = fq2_add(fq2_mul_xi(t1), t0);
   c1 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(a, b)), t0), t1);
 }
-HBX_HDNI fq12 fq12_cyclotomic_sqr(const fq12& f) {
+HBX_HD fq12 fq12_cyclotomic_sqr_i(const fq12& f) {
   fq2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
   fq2 z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   fq2 t0, t1, t2, t3;
@@ -627,6 +633,7 @@ HBX_HDNI fq12 fq12_cyclotomic_sqr(const fq12& f) {
   z3 = fq2_add(fq2_dbl(z3), t2);
   return fq12{fq6{z0, z4, z3}, fq6{z2, z1, z5}};
 }
+HBX_HDNI fq12 fq12_cyclotomic_sqr(const fq12& f) { return fq12_cyclotomic_sqr_i(f); }
 
 HBX_HD bool fq12_is_one(const fq12& a) {
   const fq12 o = fq12_one();

@@ -24,6 +24,19 @@ struct line_pre {
   fq2 c0, c1;
 };
 
+// Load of read-only data at a wave-uniform address through the constant address space, so it
+// is issued as scalar (SMEM) loads through the scalar cache: a plain global load after an
+// out-of-line call cannot be proven unclobbered and would be a vector load per lane.
+template <class T>
+HBX_HD T ld_uniform(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(4))) const T* cptr;
+  return *(cptr)p;
+#else
+  return *p;
+#endif
+}
+
 // Raw line through the doubling of T (Jacobian), scaled by 2 Y Z^3:
 //   c0 = 3X^3 - 2Y^2, c1 = -3X^2 Z^2, c2 = 2YZ^3;  T <- 2T.
 HBX_HDNI void line_dbl_step(g2j& T, fq2& c0, fq2& c1, fq2& c2) {
@@ -114,19 +127,28 @@ HBX_HDNI fq12 mul_by_line(const fq12& f, const line_pre& l, const g1a& P) {
 // Product of two Miller loops f_{|x|,QA}(PA) * f_{|x|,QB}(PB) over prepared lines, conjugated
 // for x < 0.  PA / PB are affine; a pair whose `use` flag is false contributes 1 (a pairing
 // with the identity).
-HBX_HDNI fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const line_pre* LB,
-                           const g1a& PB, bool useB) {
+// Inlined into its kernel with ONE copy each of the Fq12 squaring and the sparse line product
+// (the line loop is not unrolled): f stays in registers instead of crossing call boundaries
+// through scratch (an out-of-line Fq12 argument/result is a 576-byte scratch round trip), and
+// the line addresses stay wave-uniform (kernel argument + block index + loop counters).
+HBX_HD fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const line_pre* LB,
+                         const g1a& PB, bool useB) {
   fq12 f = fq12_one();
   int k = 0;
+#pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    if (i != 62) f = fq12_sqr(f);
-    if (useA) f = mul_by_line(f, LA[k], PA);
-    if (useB) f = mul_by_line(f, LB[k], PB);
-    k++;
-    if ((BLS_X >> i) & 1) {
-      if (useA) f = mul_by_line(f, LA[k], PA);
-      if (useB) f = mul_by_line(f, LB[k], PB);
-      k++;
+    if (i != 62) f = fq12_sqr_i(f);
+    const int steps = ((BLS_X >> i) & 1) ? 4 : 2;  // (A, B) lines of the doubling [+ addition]
+#pragma unroll 1
+    for (int s = 0; s < steps; s++) {
+      const bool b = (s & 1) != 0;
+      const line_pre L = ld_uniform((b ? LB : LA) + k);
+      if (b ? useB : useA) {
+        const fq px = b ? PB.x : PA.x;
+        const fq py = b ? PB.y : PA.y;
+        f = fq12_mul_by_014_i(f, L.c0, fq2_mul_fq(L.c1, px), py);
+      }
+      if (b) k++;
     }
   }
   return fq12_conj(f);
@@ -176,11 +198,15 @@ HBX_HDNI fq12 miller_loop_mixed(const line_pre* LA, const g1a& PA, bool useA, co
 }
 
 // g^|x| for g in the cyclotomic subgroup.
-HBX_HDNI fq12 cyc_exp_abs_x(const fq12& g) {
+// One inlined copy of the cyclotomic squaring and of the Fq12 product in a non-unrolled loop:
+// r and g stay in registers across the 63 squarings.
+HBX_HDNI fq12 cyc_exp_abs_x(const fq12& g_in) {
+  const fq12 g = g_in;
   fq12 r = g;
+#pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    r = fq12_cyclotomic_sqr(r);
-    if ((BLS_X >> i) & 1) r = fq12_mul(r, g);
+    r = fq12_cyclotomic_sqr_i(r);
+    if ((BLS_X >> i) & 1) r = fq12_mul_i(r, g);
   }
   return r;
 }
