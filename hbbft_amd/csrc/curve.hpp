@@ -117,6 +117,73 @@ HBX_HDNI g1j g1_mul_scalar(const g1j& p, const uint32_t* k8) {
   return acc;
 }
 
+// madd-2007-bl: Jacobian + affine (7M + 4S), complete for identities and P == +-Q.
+HBX_HD g1j g1_add_mixed_i(const g1j& p, const g1a& q) {
+  if (q.inf) return p;
+  if (g1j_is_identity(p)) return g1j{q.x, q.y, fq_one()};
+  const fq Z1Z1 = fq_sqr(p.z);
+  const fq U2 = fq_mul(q.x, Z1Z1);
+  const fq S2 = fq_mul(fq_mul(q.y, p.z), Z1Z1);
+  const fq H = fq_sub(U2, p.x);
+  const fq r = fq_dbl(fq_sub(S2, p.y));
+  if (fq_is_zero(H)) {
+    if (fq_is_zero(r)) return g1_dbl(p);
+    return g1_identity();
+  }
+  const fq HH = fq_sqr(H);
+  const fq I = fq_dbl(fq_dbl(HH));
+  const fq J = fq_mul(H, I);
+  const fq V = fq_mul(p.x, I);
+  const fq X3 = fq_sub(fq_sub(fq_sqr(r), J), fq_dbl(V));
+  const fq Y3 = fq_sub(fq_mul(r, fq_sub(V, X3)), fq_dbl(fq_mul(p.y, J)));
+  const fq Z3 = fq_sub(fq_sub(fq_sqr(fq_add(p.z, H)), Z1Z1), HH);
+  return g1j{X3, Y3, Z3};
+}
+
+// k * P for a 128-bit scalar (4 limbs) and affine P: one inlined doubling and one inlined mixed
+// addition in a non-unrolled loop (the accumulator stays in registers).
+HBX_HDNI g1j g1_mul_u128(const g1a& P, const uint32_t* k4) {
+  const g1a q = P;
+  g1j acc = g1_identity();
+#pragma unroll 1
+  for (int i = 127; i >= 0; i--) {
+    acc = g1_dbl(acc);
+    if ((k4[i >> 5] >> (i & 31)) & 1) acc = g1_add_mixed_i(acc, q);
+  }
+  return acc;
+}
+
+// GLV split of a canonical scalar k < r: k = k1 + k2 lambda with lambda = x^2 - 1 (128 bits),
+// k1 = k mod lambda, k2 = k div lambda (< lambda + 2 < 2^128 since r = lambda^2 + lambda + 1).
+// Then k P = k1 P + k2 phi(P), phi(x, y) = (beta x, y).
+HBX_HD void g1_glv_split(const uint32_t* k8, uint32_t* k1, uint32_t* k2) {
+  uint32_t rem[5] = {0, 0, 0, 0, 0};
+  uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 255; i >= 0; i--) {
+    // rem = 2 rem + bit
+    uint32_t c = (k8[i >> 5] >> (i & 31)) & 1u;
+#pragma unroll
+    for (int w = 0; w < 5; w++) {
+      const uint32_t nc = rem[w] >> 31;
+      rem[w] = (rem[w] << 1) | c;
+      c = nc;
+    }
+    // if rem >= lambda: rem -= lambda
+    uint32_t d[5], br = 0;
+#pragma unroll
+    for (int w = 0; w < 5; w++) d[w] = subb32(rem[w], w < 4 ? G1_GLV_LAMBDA[w] : 0u, br);
+    if (!br) {
+#pragma unroll
+      for (int w = 0; w < 5; w++) rem[w] = d[w];
+      q[i >> 5] |= 1u << (i & 31);
+    }
+  }
+  for (int w = 0; w < 4; w++) {
+    k1[w] = rem[w];
+    k2[w] = q[w];
+  }
+}
+
 // zcash compressed G1 -> affine (Montgomery).  No subgroup check.
 HBX_HDNI int32_t g1_decompress(const uint8_t* b48, g1a& out) {
   const uint8_t flags = b48[0];

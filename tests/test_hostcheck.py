@@ -107,3 +107,15 @@ def test_pairing_check_mixed_lines(hc):
     assert hc.hc_pairing_check_mixed(pa, h, ng1, sig) == 1      # e(aP, Q) e(-P, aQ) == 1
     bad = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a + 5))
     assert hc.hc_pairing_check_mixed(pa, h, ng1, bad) == 0
+
+
+def test_g1_mul_glv(hc):
+    """k_combine's two-lane GLV scalar multiplication (k1 P + k2 phi(P)) against the oracle."""
+    rnd = random.Random(7)
+    pt = bls.g1_mul(bls.G1_GEN, 0xC0FFEE)
+    comp = bls.g1_compress(pt)
+    lam = 0xd201000000010000 ** 2 - 1
+    for k in [0, 1, 2, lam - 1, lam, lam + 1, lam * lam, bls.R - 1] + [rnd.randrange(bls.R) for _ in range(8)]:
+        out = ctypes.create_string_buffer(48)
+        assert hc.hc_g1_mul_glv(comp, _be(k, 32), out) == 0
+        assert out.raw == bls.g1_compress(bls.g1_mul(pt, k)), hex(k)

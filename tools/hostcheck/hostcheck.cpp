@@ -50,6 +50,21 @@ int hc_pairing_check_mixed(const uint8_t* pa, const uint8_t* qa, const uint8_t* 
   g2_prepare_lines(QA, LA, scratch);
   return fq12_is_one(final_exponentiation(miller_loop_mixed(LA, PA, true, QB, PB, true))) ? 1 : 0;
 }
+// k * P (P compressed, k 32-byte big-endian canonical scalar) through the GLV split, as k_combine
+int hc_g1_mul_glv(const uint8_t* in48, const uint8_t* k32, uint8_t* out48) {
+  g1a p; if (g1_decompress(in48, p) != HBX_PT_OK) return -1;
+  uint32_t k8[8];
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = k32 + 28 - 4 * i;
+    k8[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  uint32_t k1[4], k2[4];
+  g1_glv_split(k8, k1, k2);
+  g1a ph = p;
+  ph.x = fq_mul(p.x, fq_from_const(G1_BETA));
+  g1j r = g1_add(g1_mul_u128(p, k1), g1_mul_u128(ph, k2));
+  g1_compress(g1_to_affine(r), out48); return 0;
+}
 int hc_g2_clear_cofactor(const uint8_t* in96, uint8_t* out96) {
   g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
   g2_compress(g2_to_affine(g2_clear_cofactor(g2_from_affine(p))), out96); return 0;
