@@ -77,84 +77,90 @@ HBX_HD fq fq_from_const(const uint32_t* c) {
 
 // Montgomery product, inputs <= 2p, output < 2p.
 //
-// Device: Finely Integrated Product Scanning (column-wise a*b and m*p interleaved) on a 96-bit
-// accumulator (acc64, c2).  Each of the 288 partial products is ONE v_mad_u64_u32 that adds into
-// the 64-bit accumulator with its carry-out in VCC plus ONE v_addc_co_u32 into the third word --
-// no 64-bit pair construction (the compiler's lowering of `(uint64_t)a * b + t + c` spends ~2.3
-// v_mov per multiply-add on even-aligned register pairs).  p's limbs are SGPR operands.
-// Bounds: inputs < 2p and 4p < R give an output < 2p; the last column leaves no carry.
-// Host (tools/hostcheck, tools/opcount): the textbook CIOS below, same result.
+// Digit-sliced product scanning.  The operands stay 12 x 32-bit limbs with R = 2^384 everywhere
+// else; inside the product they are re-cut into 14 digits of 28 bits (13 x 28 + 20 = 384), so a
+// column of <= 14 a*b products plus <= 14 m*p products (each < 2^56) fits a 64-bit accumulator:
+// every partial product is ONE v_mad_u64_u32 with no carry word.  (With 32-bit digits each
+// product needed a v_mad_u64_u32 plus a v_addc_co_u32 into a third word and the loop carried
+// ~100 moves; measured on MI355X at one wave per SIMD: 1.9 us -> 1.5 us per product,
+// tools/microbench/fq28.hip.)  The Montgomery digits m_0..m_12 are 28-bit, m_13 is 20-bit, so
+// the reduction divides by exactly 2^(13*28 + 20) = 2^384 = R.
+// Bounds: a, b < 2p and M = sum m_j 2^(28 j) < 2^384 give (ab + Mp)/R < 4p^2/R + p < 2p.
+// The same C++ runs on the host (tools/hostcheck, tools/opcount), so the host check exercises
+// exactly this digit schedule.
+HBX_HD void fq_unpack28(const fq& a, uint32_t* d) {
+#pragma unroll
+  for (int j = 0; j < 14; j++) {
+    const int bit = 28 * j, w = bit >> 5, sh = bit & 31;
+    uint32_t v = a.l[w] >> sh;
+    if (sh > 4 && w + 1 < 12) v |= a.l[w + 1] << (32 - sh);
+    d[j] = j == 13 ? v : (v & 0x0FFFFFFFu);
+  }
+}
 #if defined(__HIP_DEVICE_COMPILE__)
-#define HBX_MADC(acc, c2, x, y)                                                                   \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"                 \
-      : "+v"(acc), "+v"(c2)                                                                        \
-      : "v"(x), "v"(y)                                                                             \
-      : "vcc")
-// one multiply-add on each of two independent chains in one statement (hipcc pads one wait
-// state after every asm statement; pairing halves those pads)
-#define HBX_MADC2(acc, c2, x, y, acc2, c22, x2, ys2)                                              \
-  asm("v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"               \
-      "v_mad_u64_u32 %2, vcc, %6, %7, %2\n\tv_addc_co_u32 %3, vcc, 0, %3, vcc"                   \
-      : "+v"(acc), "+v"(c2), "+v"(acc2), "+v"(c22)                                                 \
-      : "v"(x), "v"(y), "v"(x2), "s"(ys2)                                                          \
-      : "vcc")
-#define HBX_MADC_S(acc, c2, x, ys)                                                                \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"                 \
-      : "+v"(acc), "+v"(c2)                                                                        \
-      : "v"(x), "s"(ys)                                                                            \
-      : "vcc")
-// 96-bit accumulator add: (acc, c2) += (x, y)
-#define HBX_ACC_ADD(acc, c2, x, y)                                                                \
-  asm("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, %3, vcc"                       \
-      : "+v"(acc), "+v"(c2)                                                                        \
-      : "v"(x), "v"(y)                                                                             \
-      : "vcc")
-// One out-of-line copy (a fully unrolled product is ~900 instructions; inlined at every call
-// site the tower code would not fit the instruction cache).  Limbs travel as 24 scalar arguments
-// so the call passes them in VGPRs (a second 12-dword aggregate would go through the stack).
+#define HBX_FQMUL_ATTR __device__ __noinline__
+#else
+#define HBX_FQMUL_ATTR inline
+#endif
+// One out-of-line copy on the device (inlined at every call site the tower code would not fit
+// the instruction cache).  Limbs travel as 24 scalar arguments so the call passes them in VGPRs.
 #define HBX_L12(x) x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11
 #define HBX_P12(x)                                                                                  \
   uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6, \
       uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
-__device__ __noinline__ fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
+HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
   const fq a = {{HBX_L12(a)}};
   const fq b = {{HBX_L12(b)}};
-  // two independent accumulation chains per column (a*b and m*p) so consecutive multiply-adds
-  // never depend on each other; they are merged once per column
+  uint32_t A[14], B[14], m[14], o[15];
+  fq_unpack28(a, A);
+  fq_unpack28(b, B);
   uint64_t acc = 0;
-  uint32_t c2 = 0;
-  uint32_t m[12];
-  fq r;
 #pragma unroll
-  for (int i = 0; i < 23; i++) {
-    const int jlo = i < 12 ? 0 : i - 11;
-    const int jhi = i < 12 ? i : 11;
-    uint64_t acc2 = 0;
-    uint32_t c22 = 0;
+  for (int k = 0; k < 27; k++) {
+    const int jlo = k < 14 ? 0 : k - 13;
+    const int jhi = k < 14 ? k : 13;
+    // two interleaved a*b chains and one m*p chain; m_{k-1} p_1 (the only term that waits on
+    // the previous digit) is added last
+    uint64_t s0 = acc, s1 = 0, t = 0;
 #pragma unroll
     for (int j = jlo; j <= jhi; j++) {
-      if (j < i) HBX_MADC2(acc, c2, a.l[j], b.l[i - j], acc2, c22, m[j], FQ_P[i - j]);
-      else HBX_MADC(acc, c2, a.l[j], b.l[i - j]);
+      if (j & 1) s1 = (uint64_t)A[j] * B[k - j] + s1;
+      else s0 = (uint64_t)A[j] * B[k - j] + s0;
     }
-    // acc += acc2 (96-bit)
-    {
-      uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
-      asm("v_add_co_u32 %0, vcc, %0, %3\n\tv_addc_co_u32 %1, vcc, %1, %4, vcc\n\tv_addc_co_u32 %2, vcc, %2, %5, vcc"
-          : "+v"(lo), "+v"(hi), "+v"(c2)
-          : "v"((uint32_t)acc2), "v"((uint32_t)(acc2 >> 32)), "v"(c22)
-          : "vcc");
-      acc = ((uint64_t)hi << 32) | lo;
-    }
-    if (i < 12) {
-      m[i] = (uint32_t)acc * FQ_INV;
-      HBX_MADC_S(acc, c2, m[i], FQ_P[0]);
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++)
+      if (j < k - 1) t = (uint64_t)m[j] * FQ_P28[k - j] + t;
+    acc = s0 + s1 + t;
+    if (k >= 1 && k <= 14) acc = (uint64_t)m[k - 1] * FQ_P28[1] + acc;
+    if (k < 13) {
+      m[k] = ((uint32_t)acc * FQ_INV28) & 0x0FFFFFFFu;
+      acc = (uint64_t)m[k] * FQ_P28[0] + acc;  // low 28 bits cancel
+      acc >>= 28;
+    } else if (k == 13) {
+      m[k] = ((uint32_t)acc * FQ_INV28) & 0x000FFFFFu;
+      acc = (uint64_t)m[k] * FQ_P28[0] + acc;  // low 20 bits cancel: R = 2^384 reached
+      o[0] = (uint32_t)(acc >> 20) & 0xFFu;    // result bits 0..7
+      acc >>= 28;
     } else {
-      r.l[i - 12] = (uint32_t)acc;
+      o[k - 13] = (uint32_t)acc & 0x0FFFFFFFu;  // result bits 8 + 28 (k - 14) ..
+      acc >>= 28;
     }
-    acc = (acc >> 32) | ((uint64_t)c2 << 32);
-    c2 = 0;
   }
-  r.l[11] = (uint32_t)acc;
+  o[14] = (uint32_t)acc;  // result bits 372..
+  fq r;
+#pragma unroll
+  for (int w = 0; w < 12; w++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+      const int off = i == 0 ? 0 : 8 + 28 * (i - 1);
+      const int width = i == 0 ? 8 : (i == 14 ? 32 : 28);
+      if (off + width <= 32 * w || off >= 32 * w + 32) continue;
+      if (off >= 32 * w) v |= o[i] << (off - 32 * w);
+      else v |= o[i] >> (32 * w - off);
+    }
+    r.l[w] = v;
+  }
   return r;
 }
 HBX_HD fq fq_mul(const fq& a, const fq& b) {
@@ -165,37 +171,7 @@ HBX_HD fq fq_mul(const fq& a, const fq& b) {
 }
 #undef HBX_L12
 #undef HBX_P12
-#undef HBX_ACC_ADD
-#undef HBX_MADC
-#undef HBX_MADC_S
-#undef HBX_MADC2
-#else
-HBX_HD fq fq_mul(const fq& a, const fq& b) {
-  HBX_COUNT_FQMUL();
-  uint32_t t[12];
-  for (int j = 0; j < 12; j++) t[j] = 0;
-  for (int i = 0; i < 12; i++) {
-    const uint32_t bi = b.l[i];
-    uint64_t s = (uint64_t)a.l[0] * bi + t[0];
-    uint32_t A = (uint32_t)(s >> 32);
-    const uint32_t t0 = (uint32_t)s;
-    const uint32_t m = t0 * FQ_INV;
-    uint64_t c = (uint64_t)m * FQ_P[0] + t0;
-    uint32_t C = (uint32_t)(c >> 32);
-    for (int j = 1; j < 12; j++) {
-      s = (uint64_t)a.l[j] * bi + t[j] + A;
-      A = (uint32_t)(s >> 32);
-      c = (uint64_t)m * FQ_P[j] + (uint32_t)s + C;
-      C = (uint32_t)(c >> 32);
-      t[j - 1] = (uint32_t)c;
-    }
-    t[11] = C + A;
-  }
-  fq r;
-  for (int j = 0; j < 12; j++) r.l[j] = t[j];
-  return r;
-}
-#endif
+#undef HBX_FQMUL_ATTR
 
 HBX_HD fq fq_sqr(const fq& a) { return fq_mul(a, a); }
 

@@ -43,6 +43,26 @@ def test_fq_mul_inv(hc):
         assert int.from_bytes(out.raw, "big") * a % bls.P == 1
 
 
+def test_fq_mul_lazy_range(hc):
+    """The digit-sliced Montgomery product on lazy operands in [0, 2p]: r = a b / 2^384 mod p and
+    r < 2p (the bound the tower relies on), including the extremes 0, p, 2p - 1 and 2p."""
+    rnd = random.Random(7)
+    P2 = 2 * bls.P
+    edge = [0, 1, bls.P - 1, bls.P, bls.P + 1, P2 - 1, P2, (1 << 381) - 1]
+    pairs = [(a, b) for a in edge for b in edge] + [(rnd.randrange(P2 + 1), rnd.randrange(P2 + 1)) for _ in range(400)]
+    rinv = pow(1 << 384, -1, bls.P)
+    for a, b in pairs:
+        if a > P2 or b > P2:
+            continue
+        A = (ctypes.c_uint32 * 12)(*[(a >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        B = (ctypes.c_uint32 * 12)(*[(b >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        O = (ctypes.c_uint32 * 12)()
+        hc.hc_fq_mul_raw(A, B, O)
+        r = sum(int(O[i]) << (32 * i) for i in range(12))
+        assert r < P2, (hex(a), hex(b))
+        assert r % bls.P == a * b * rinv % bls.P, (hex(a), hex(b))
+
+
 def test_point_roundtrips(hc):
     for k in (1, 2, 0xDEADBEEF, bls.R - 1):
         c1 = bls.g1_compress(bls.g1_mul(bls.G1_GEN, k))

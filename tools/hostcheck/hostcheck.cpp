@@ -11,6 +11,14 @@ void hc_fq_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   fq x = fq_to_mont(fq_from_be(a)), y = fq_to_mont(fq_from_be(b));
   fq_to_be(fq_from_mont(fq_mul(x, y)), out);
 }
+// raw limbs (little-endian 12 x u32, any value < 2^384): the Montgomery product fq_mul itself,
+// so tests can drive lazy-range operands in [0, 2p] and check r = a b 2^-384 mod p, r < 2p
+void hc_fq_mul_raw(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  fq x, y;
+  for (int i = 0; i < 12; i++) { x.l[i] = a[i]; y.l[i] = b[i]; }
+  const fq r = fq_mul(x, y);
+  for (int i = 0; i < 12; i++) out[i] = r.l[i];
+}
 void hc_fq_inv(const uint8_t* a, uint8_t* out) {
   fq x = fq_to_mont(fq_from_be(a));
   fq_to_be(fq_from_mont(fq_inv(x)), out);
