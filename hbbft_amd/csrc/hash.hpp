@@ -208,6 +208,67 @@ HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
   }
 }
 
+#if defined(__HIPCC__)
+// hash_g2 by a GROUP of K aligned lanes of one wave (K | 64), same point as g2_rand_from_rng.
+//
+// Why.  One lane per hash leaves a wave waiting for its unluckiest lane: every lane draws
+// candidates x from the ChaCha stream until x^3 + b is a square (probability 1/2 each), so a wave
+// runs ~log2(64) + 1 residuosity exponentiations instead of the 2 a lane needs on average.  Here
+// lane g of the group draws the stream itself (cheap) but tests only candidate base + g, all K tests
+// run as ONE exponentiation, and the lowest passing index wins -- exactly the candidate the
+// sequential loop would stop at.  Only the winner lane runs the square root and the cofactor
+// clearing.  A cleared point equal to the identity makes the sequential loop continue with the next
+// candidate; so does this one (base = winner + 1).  `active` must be group-uniform.
+// Returns true on the lane that holds the result in `out`.
+template <int K>
+__device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
+  static_assert(K >= 2 && K <= 32 && (64 % K) == 0, "group size");
+  if (!active) return false;
+  const int lane = (int)(threadIdx.x & 63);
+  const int gl = lane % K;
+  const int gbase = lane - gl;
+  const uint64_t gmask = ((1ull << K) - 1) << gbase;
+  chacha_rng r;
+  chacha_rng_from_digest(r, d32);
+  uint32_t drawn = 0, base = 0;
+  fq2 x = fq2_zero();
+  bool greatest = false;
+  for (;;) {
+    // draw up to candidate base + gl (monotone: base only grows)
+    while (drawn <= base + (uint32_t)gl) {
+      const fq c0 = fq_rand(r);
+      const fq c1 = fq_rand(r);
+      x = fq2{c0, c1};
+      greatest = (chacha_next_u32(r) & 1u) != 0;
+      drawn++;
+    }
+    const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+    const bool c1zero = fq_is_zero(rhs.c1);
+    fq s = fq_zero();
+    fq2 y0 = fq2_zero();
+    bool sq;
+    if (c1zero) sq = fq2_sqrt(rhs, y0);  // measure-zero branch, exact general square root
+    else sq = fq2_norm_sqrt(rhs, s);
+    const uint64_t pass = __ballot(sq) & gmask;
+    if (pass == 0) {
+      base += K;
+      continue;
+    }
+    const int win = __builtin_ctzll(pass) - gbase;
+    bool ident = false;
+    if (gl == win) {
+      fq2 y = c1zero ? y0 : fq2_sqrt_from_norm(rhs, s);
+      // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
+      if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
+      out = g2_clear_cofactor(g2j{x, y, fq2_one()});
+      ident = g2j_is_identity(out);
+    }
+    if ((__ballot(ident) & gmask) == 0) return gl == win;
+    base += (uint32_t)win + 1;
+  }
+}
+#endif
+
 // hash_g2(digest) where the digest is already computed.
 HBX_HD g2j hash_g2_from_digest(const uint8_t* d32) {
   chacha_rng r;
@@ -216,8 +277,7 @@ HBX_HD g2j hash_g2_from_digest(const uint8_t* d32) {
 }
 
 // hash_g1_g2(u, v): m = (|v| > 64 ? SHA256(v) : v) || u_comp48; H = hash_g2(m).
-HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen) {
-  uint8_t d[32];
+HBX_HD void hash_g1_g2_digest(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen, uint8_t* d) {
   if (vlen > 64) {
     uint8_t dv[32];
     sha256_2(v, vlen, nullptr, 0, dv);
@@ -225,6 +285,10 @@ HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen) 
   } else {
     sha256_2(v, vlen, u_comp48, 48, d);
   }
+}
+HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen) {
+  uint8_t d[32];
+  hash_g1_g2_digest(u_comp48, v, vlen, d);
   return hash_g2_from_digest(d);
 }
 

@@ -54,7 +54,7 @@ struct hbx_ctx {
   dbuf pk, pk_status, pk_comp;
   // epoch state
   uint32_t p_ct = 0;
-  dbuf U, G2pts, lines, scratch, ct_ok, ct_valid;
+  dbuf U, G2pts, lines, scratch, ct_ok, ct_valid, dec_st;
   bool ct_known = false;  // ct_valid computed (else deferred into the next share verification)
   const uint8_t* d_v_blob = nullptr;  // device V blob used by the combine (caller-owned for _d)
   const uint64_t* d_v_off = nullptr;
@@ -381,19 +381,22 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) ||
       !c->lines.ensure((size_t)p * sizeof(line_block)) ||
       !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
-      !c->ct_valid.ensure(p))
+      !c->ct_valid.ensure(p) || !c->dec_st.ensure((size_t)2 * p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
   const dim3 b64(64);
   {
     timed t_(c, HBX_K_PREPARE_CT, s);
-    hipLaunchKernelGGL(k_prepare_ct, dim3((p + 63) / 64), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p,
-                       c->U.as<g1a>(), c->G2pts.as<g2a>(), c->ct_ok.as<uint8_t>());
+    const uint32_t hash_blocks = (uint32_t)(((size_t)p * HASH_K + 63) / 64);
+    const uint32_t dec_blocks = (2 * p + 63) / 64;
+    hipLaunchKernelGGL(k_prepare_ct, dim3(hash_blocks + dec_blocks), b64, 0, s, d_u_comp, d_v_blob, d_v_off,
+                       d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>());
   }
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
-                       c->lines.as<line_pre>(), c->scratch.as<fq2>());
+                       c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
+                       c->ct_ok.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());
   c->p_ct = p;
@@ -593,14 +596,14 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   HIPCHK(c, hipMemcpyAsync(c->coin_off.p, nonce_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
   {
     timed t_(c, HBX_K_HASH_NONCES, s);
-    hipLaunchKernelGGL(k_hash_nonces, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
+    hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
                        c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>());
   }
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
-                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>());
+                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr);
   }
   HIPCHK(c, hipGetLastError());
   if (h96) {

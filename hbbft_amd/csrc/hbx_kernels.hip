@@ -43,41 +43,71 @@ __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict_
   status[i] = st;
 }
 
-// One lane per proposer: decode U_j and W_j, compute H_j = hash_g1_g2(U_j, V_j).
+// Lanes per hash_g2 group (hash.hpp hash_g2_group).
+constexpr int HASH_K = 16;
+
+// H_j = hash_g1_g2(U_j, V_j) for every proposer, plus the decoding of U_j and W_j, in ONE launch:
+//  * blocks [0, hash_blocks): HASH_K-lane groups, one per proposer (hash_g2_group); the hash reads
+//    only the compressed bytes of U_j, so it does not wait for the decode;
+//  * blocks [hash_blocks, ...): one lane per point decodes U_j (j < p) or W_j (p <= j < 2p), in
+//    waves of their own, concurrently with the hash waves.
+// ct_ok and the identity substitution for undecodable ciphertexts (H_j = O) are applied by
+// k_prepare_lines, which runs after both.
 __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u_comp,
                                                    const uint8_t* __restrict__ v_blob,
                                                    const uint64_t* __restrict__ v_off,
                                                    const uint8_t* __restrict__ w_comp, uint32_t p,
-                                                   g1a* __restrict__ U, g2a* __restrict__ G2pts,
-                                                   uint8_t* __restrict__ ct_ok) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= p) return;
-  g1a u;
-  g2a w;
-  const int32_t su = g1_decompress(u_comp + (size_t)j * 48, u);
-  const int32_t sw = g2_decompress(w_comp + (size_t)j * 96, w);
-  const bool ok = (su == HBX_PT_OK || su == HBX_PT_INFINITY) && (sw == HBX_PT_OK || sw == HBX_PT_INFINITY);
-  g2a h;
-  h.x = fq2_zero();
-  h.y = fq2_zero();
-  h.inf = true;
-  if (ok) {
-    const uint64_t off = v_off[j];
-    const uint64_t len = v_off[j + 1] - off;
-    h = g2_to_affine(hash_g1_g2(u_comp + (size_t)j * 48, v_blob + off, len));
+                                                   uint32_t hash_blocks, g1a* __restrict__ U,
+                                                   g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st) {
+  if (blockIdx.x >= hash_blocks) {
+    const uint32_t k = (blockIdx.x - hash_blocks) * blockDim.x + threadIdx.x;
+    if (k < p) {
+      g1a u;
+      dec_st[k] = g1_decompress(u_comp + (size_t)k * 48, u);
+      U[k] = u;
+    } else if (k < 2 * p) {
+      const uint32_t j = k - p;
+      g2a w;
+      dec_st[k] = g2_decompress(w_comp + (size_t)j * 96, w);
+      G2pts[2 * j + 1] = w;
+    }
+    return;
   }
-  U[j] = u;
-  G2pts[2 * j] = h;
-  G2pts[2 * j + 1] = w;
-  ct_ok[j] = ok ? 1 : 0;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = gid / HASH_K;
+  if (j >= p) return;  // whole groups only (HASH_K | 64)
+  const uint64_t off = v_off[j];
+  const uint64_t len = v_off[j + 1] - off;
+  uint8_t d[32];
+  hash_g1_g2_digest(u_comp + (size_t)j * 48, v_blob + off, len, d);
+  g2j h;
+  if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
 }
 
-// One lane per G2 point: the 68 normalised lines.
-__global__ void __launch_bounds__(64) k_prepare_lines(const g2a* __restrict__ pts, uint32_t count,
-                                                      line_pre* __restrict__ lines, fq2* __restrict__ scratch) {
+// One lane per G2 point: the 68 normalised lines.  With `dec_st` (ciphertext points), lane 2j also
+// settles ct_ok[j]: U_j and W_j must decode (threshold_crypto deserialisation); otherwise H_j is
+// replaced by the identity and the proposer's checks are gated off.
+__global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
+                                                      line_pre* __restrict__ lines, fq2* __restrict__ scratch,
+                                                      const int32_t* __restrict__ dec_st, uint32_t p,
+                                                      uint8_t* __restrict__ ct_ok) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
-  const g2a q = pts[k];
+  g2a q = pts[k];
+  if (dec_st) {
+    const uint32_t j = k >> 1;
+    const int32_t su = dec_st[j], sw = dec_st[p + j];
+    const bool ok = (su == HBX_PT_OK || su == HBX_PT_INFINITY) && (sw == HBX_PT_OK || sw == HBX_PT_INFINITY);
+    if ((k & 1) == 0) {
+      ct_ok[j] = ok ? 1 : 0;
+      if (!ok) {
+        q.x = fq2_zero();
+        q.y = fq2_zero();
+        q.inf = true;
+        pts[k] = q;
+      }
+    }
+  }
   if (q.inf) {
     for (int i = 0; i < MILLER_LINES; i++) {
       lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
@@ -450,14 +480,16 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
 // ----------------------------------------------------------------------------------------------
 // Common Coin (reference src/common_coin.rs)
 // ----------------------------------------------------------------------------------------------
-// H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one lane each.
+// H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one HASH_K-lane
+// group each.
 __global__ void __launch_bounds__(64) k_hash_nonces(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
                                                     uint32_t count, g2a* __restrict__ H) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= count) return;
+  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / HASH_K;
+  if (j >= count) return;  // whole groups only
   uint8_t d[32];
   sha256_2(blob + off[j], off[j + 1] - off[j], nullptr, 0, d);
-  H[j] = g2_to_affine(hash_g2_from_digest(d));
+  g2j h;
+  if (hash_g2_group<HASH_K>(d, true, h)) H[j] = g2_to_affine(h);
 }
 
 __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict__ comp, size_t count,
