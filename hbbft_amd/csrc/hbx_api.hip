@@ -748,6 +748,27 @@ int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* 
   return HBX_OK;
 }
 
+int hbx_decrypt_epoch_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob, const uint64_t* d_v_off,
+                        const uint8_t* d_w_comp, uint32_t p, uint64_t max_v_len, const uint8_t* d_shares,
+                        const uint8_t* d_present, uint32_t n, uint32_t t, uint8_t* d_valid, uint8_t* d_ct_valid,
+                        uint8_t* d_out_blob, int32_t* d_status, void* stream) {
+  if (!c || !d_shares || n == 0 || p == 0 || t == 0 || t > (uint32_t)COMBINE_MAX_T || !d_out_blob)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_epoch_d: bad args");
+  if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
+  // Stages in stream order.  (Running Ciphertext::verify on the aux stream beside a speculative
+  // combine was measured on MI355X and gained nothing: the combine's 4 waves per proposer already
+  // occupy every SIMD, and two single-wave-per-SIMD kernels only time-share the VALU.)
+  int rc = hbx_prepare_ciphertexts_d(c, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, max_v_len, nullptr, stream);
+  if (rc) return rc;
+  rc = hbx_verify_dec_shares_d(c, d_shares, d_present, n, p, d_valid, stream);
+  if (rc) return rc;
+  if (d_ct_valid) {
+    rc = hbx_get_ct_valid_d(c, d_ct_valid, stream);
+    if (rc) return rc;
+  }
+  return hbx_combine_decrypt_d(c, t, d_out_blob, d_status, stream);
+}
+
 int hbx_combine_decrypt(hbx_ctx* c, uint32_t t, uint8_t* out_blob, int32_t* status) {
   if (!c || !out_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt: bad args");
   HIPCHK(c, hipSetDevice(c->device));

@@ -189,8 +189,9 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   }
   __syncthreads();
   const int count = s_count;
-  if (!ct_valid[j] || count < (int)t) {
-    if (tid == 0) status[j] = !ct_valid[j] ? -7 : -3;
+  const bool ctv = ct_valid[j] != 0;
+  if (!ctv || count < (int)t) {
+    if (tid == 0) status[j] = !ctv ? -7 : -3;
     return;
   }
   // two lanes per share (GLV): lane 2k computes k1 S_k, lane 2k+1 computes k2 phi(S_k) with

@@ -42,6 +42,7 @@ EXPORTS = (
     "hbx_verify_dec_shares_d",
     "hbx_combine_decrypt_d",
     "hbx_get_ct_valid_d",
+    "hbx_decrypt_epoch_d",
     "hbx_public_keys",
     "hbx_encrypt",
     "hbx_decrypt_shares",
@@ -97,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_verify_dec_shares_d.argtypes = [P, P, P, u32, u32, P, P]
     lib.hbx_combine_decrypt_d.argtypes = [P, u32, P, P, P]
     lib.hbx_get_ct_valid_d.argtypes = [P, P, P]
+    lib.hbx_decrypt_epoch_d.argtypes = [P, P, P, P, P, u32, ctypes.c_uint64, P, P, u32, u32, P, P, P, P, P]
     lib.hbx_prepare_nonces.argtypes = [P, u8p, u64p, u32, u8p]
     lib.hbx_sign.argtypes = [P, u8p, u32, u8p]
     lib.hbx_verify_sig_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
@@ -339,3 +341,13 @@ class Context:
     def combine_decrypt_d(self, t: int, d_out, d_status=None, stream=None):
         self._check(self.lib.hbx_combine_decrypt_d(
             self.h, t, d_out.data_ptr(), None if d_status is None else d_status.data_ptr(), stream))
+
+    def decrypt_epoch_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_shares, n: int, t: int, d_out,
+                        d_valid=None, d_ct_valid=None, d_status=None, d_present=None, stream=None):
+        """One node-epoch (hbx_decrypt_epoch_d): prepare + share checks + Ciphertext::verify beside the
+        speculative combine + decrypt; same results as the three-call sequence."""
+        opt = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        self._check(self.lib.hbx_decrypt_epoch_d(
+            self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
+            d_shares.data_ptr(), opt(d_present), n, t, opt(d_valid), opt(d_ct_valid), d_out.data_ptr(),
+            opt(d_status), stream))

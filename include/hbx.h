@@ -141,6 +141,17 @@ int hbx_combine_decrypt_d(hbx_ctx* ctx, uint32_t t, uint8_t* d_out_blob, int32_t
                           void* stream);
 int hbx_get_ct_valid_d(hbx_ctx* ctx, uint8_t* d_ct_valid, void* stream);
 
+/* One node-epoch of threshold decryption in ONE call: what honey_badger.rs does per epoch through
+ * Ciphertext::verify (:371), verify_decryption_share (:229, :422-444) and PublicKeySet::decrypt
+ * (:340), batched ("route whole epochs' worth of shares through one batched call").
+ * Results and stream semantics are those of hbx_prepare_ciphertexts_d (Ciphertext::verify
+ * deferred) + hbx_verify_dec_shares_d + hbx_get_ct_valid_d + hbx_combine_decrypt_d.
+ * All outputs are device arrays, complete when `stream` reaches the end of the call's work. */
+int hbx_decrypt_epoch_d(hbx_ctx* ctx, const uint8_t* d_u_comp, const uint8_t* d_v_blob, const uint64_t* d_v_off,
+                        const uint8_t* d_w_comp, uint32_t p, uint64_t max_v_len, const uint8_t* d_shares,
+                        const uint8_t* d_present, uint32_t n, uint32_t t, uint8_t* d_valid, uint8_t* d_ct_valid,
+                        uint8_t* d_out_blob, int32_t* d_status, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Producer side.  Scalars are canonical Fr values as
  * 32-byte big-endian strings (< r; anything else is HBX_E_INVALID_ARG).

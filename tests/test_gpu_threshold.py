@@ -34,3 +34,40 @@ def test_epoch_matches_golden(hbx_ctx, n):
     for j, pt in enumerate(plains):
         if status[j] == 0:
             assert pt == d["expect_plain_blob"][int(off[j]):int(off[j + 1])].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 7])
+def test_fused_epoch_call_matches_golden(hbx_ctx, n):
+    """hbx_decrypt_epoch_d (Ciphertext::verify on the second stream beside the speculative
+    combine) gives the fixture's bits, statuses and plaintexts, invalid ciphertext included."""
+    import torch
+
+    d = _load(n)
+    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
+    dev = torch.device("cuda", 0)
+    p = len(d["v_off"]) - 1
+    nn = d["shares"].shape[1]
+    off = d["v_off"].astype(np.int64)
+    t_u = torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev)
+    t_w = torch.from_numpy(np.ascontiguousarray(d["w"])).to(dev)
+    t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"]).astype(np.uint8).copy() if len(d["v_blob"]) else np.zeros(1, np.uint8)).to(dev)
+    t_off = torch.from_numpy(off).to(dev)
+    t_sh = torch.from_numpy(np.ascontiguousarray(d["shares"])).to(dev)
+    t_pr = torch.from_numpy(np.ascontiguousarray(d["present"]).astype(np.uint8)).to(dev)
+    t_out = torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
+    t_valid = torch.zeros(p * nn, dtype=torch.uint8, device=dev)
+    t_ct = torch.zeros(p, dtype=torch.uint8, device=dev)
+    t_st = torch.zeros(p, dtype=torch.int32, device=dev)
+    maxv = int(np.max(np.diff(off))) if p else 0
+    hbx_ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, p, maxv, t_sh, nn, int(d["t"]), t_out, d_valid=t_valid,
+                            d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(t_ct.cpu().numpy(), d["expect_ct_valid"])
+    np.testing.assert_array_equal(t_valid.cpu().numpy().reshape(p, nn), d["expect_valid"].reshape(p, nn))
+    status = t_st.cpu().numpy()
+    np.testing.assert_array_equal(status, d["expect_status"])
+    out = t_out.cpu().numpy()
+    for j in range(p):
+        if status[j] == 0:
+            assert out[off[j]:off[j + 1]].tobytes() == d["expect_plain_blob"][int(off[j]):int(off[j + 1])].tobytes()
