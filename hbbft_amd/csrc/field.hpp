@@ -163,8 +163,51 @@ HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
   }
   return r;
 }
+#if defined(HBX_HOST_INT128) && !defined(__HIPCC__)
+// Host-only alternative for the CPU baseline port (tools/cpu_baseline): textbook 6 x 64-bit CIOS
+// with unsigned __int128, the limb shape pairing 0.14 (u128-support) uses on x86-64.  Same
+// Montgomery value (R = 2^384, output < 2p); the GPU and tools/hostcheck never use it.
+inline fq fq_mul_cios64(const fq& a, const fq& b) {
+  typedef unsigned __int128 u128;
+  uint64_t A[6], B[6], P6[6], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 6; i++) {
+    A[i] = (uint64_t)a.l[2 * i] | ((uint64_t)a.l[2 * i + 1] << 32);
+    B[i] = (uint64_t)b.l[2 * i] | ((uint64_t)b.l[2 * i + 1] << 32);
+    P6[i] = (uint64_t)FQ_P[2 * i] | ((uint64_t)FQ_P[2 * i + 1] << 32);
+  }
+  const uint64_t pinv = 0x89f3fffcfffcfffdull;  // -p^-1 mod 2^64
+  for (int i = 0; i < 6; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 6; j++) {
+      c = (u128)A[j] * B[i] + t[j] + (uint64_t)(c >> 64);
+      t[j] = (uint64_t)c;
+    }
+    u128 s = (u128)t[6] + (uint64_t)(c >> 64);
+    t[6] = (uint64_t)s;
+    t[7] = (uint64_t)(s >> 64);
+    const uint64_t m = t[0] * pinv;
+    c = (u128)m * P6[0] + t[0];
+    for (int j = 1; j < 6; j++) {
+      c = (u128)m * P6[j] + t[j] + (uint64_t)(c >> 64);
+      t[j - 1] = (uint64_t)c;
+    }
+    s = (u128)t[6] + (uint64_t)(c >> 64);
+    t[5] = (uint64_t)s;
+    t[6] = t[7] + (uint64_t)(s >> 64);
+  }
+  fq r;
+  for (int i = 0; i < 6; i++) {
+    r.l[2 * i] = (uint32_t)t[i];
+    r.l[2 * i + 1] = (uint32_t)(t[i] >> 32);
+  }
+  return r;
+}
+#endif
 HBX_HD fq fq_mul(const fq& a, const fq& b) {
   HBX_COUNT_FQMUL();
+#if defined(HBX_HOST_INT128) && !defined(__HIPCC__)
+  return fq_mul_cios64(a, b);
+#endif
   return fq_mul_limbs(a.l[0], a.l[1], a.l[2], a.l[3], a.l[4], a.l[5], a.l[6], a.l[7], a.l[8], a.l[9], a.l[10],
                       a.l[11], b.l[0], b.l[1], b.l[2], b.l[3], b.l[4], b.l[5], b.l[6], b.l[7], b.l[8], b.l[9],
                       b.l[10], b.l[11]);

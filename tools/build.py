@@ -50,7 +50,21 @@ def build_oracle(force=False):
     return out
 
 
+def build_cpu_port(force=False):
+    """CPU baseline (bench.py cpu_baseline leg only): the reference's per-share algorithm shape."""
+    src = os.path.join(ROOT, "tools", "cpu_baseline", "cpu_port.cpp")
+    hdrs = glob.glob(os.path.join(ROOT, "hbbft_amd", "csrc", "*.hpp"))
+    outdir = os.path.join(ROOT, "oracle", "_build")
+    os.makedirs(outdir, exist_ok=True)
+    out = os.path.join(outdir, "libcpu_port.so")
+    if not force and newer(out, [src] + hdrs):
+        return out
+    run(["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", out, src])
+    return out
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     build_hbx(force)
     build_oracle(force)
+    build_cpu_port(force)

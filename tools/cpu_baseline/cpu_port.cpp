@@ -1,0 +1,87 @@
+// CPU baseline ("port"): threshold_crypto's PublicKeyShare::verify_decryption_share in the shape the
+// reference runs it (honey_badger.rs:229 -> threshold_crypto -> pairing 0.14), timed on host cores.
+// Per share, exactly as the reference does it:
+//   * H = hash_g1_g2(U, V) recomputed for every share, with pairing 0.14's scale_by_cofactor shape
+//     (507-bit double-and-add of h2, not the kernels' psi shortcut);
+//   * two independent pairings e(S, H) and e(pk_i, W), each = G2 line preparation + Miller loop +
+//     its own final exponentiation, compared in Fq12.
+// The tower/curve code is the kernels' __host__ __device__ C++ compiled by g++; the Fq product is the
+// 6 x 64-bit __int128 CIOS (HBX_HOST_INT128), the limb shape pairing 0.14 uses on x86-64.
+// std::thread spreads independent shares over host cores (the reference is single-threaded per
+// node; the thread count is reported).  NOT part of the product; built by tools/build.py into
+// oracle/_build/ and loaded only by bench.py's cpu_baseline leg.
+#include <atomic>
+#include <cstring>
+#include <thread>
+#define HBX_HOST_INT128 1
+#include <vector>
+#include "../../hbbft_amd/csrc/pairing.hpp"
+#include "../../hbbft_amd/csrc/hash.hpp"
+using namespace hbx;
+
+namespace {
+// G2::rand + scale_by_cofactor as pairing 0.14 computes it (h2 * P by double-and-add).
+g2j g2_rand_reference_shape(chacha_rng& r) {
+  for (;;) {
+    const fq c0 = fq_rand(r);
+    const fq c1 = fq_rand(r);
+    const fq2 x{c0, c1};
+    const bool greatest = (chacha_next_u32(r) & 1u) != 0;
+    const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
+    fq2 y;
+    if (!fq2_sqrt(rhs, y)) continue;
+    if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
+    const g2j p = g2_mul_bits(g2j{x, y, fq2_one()}, G2_COFACTOR, G2_COFACTOR_BITS);
+    if (!g2j_is_identity(p)) return p;
+  }
+}
+fq12 pairing(const g1a& P, const g2a& Q) {
+  line_pre L[MILLER_LINES];
+  fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(Q, L, scratch);
+  return final_exponentiation(miller_loop2(L, P, true, L, P, false));
+}
+bool fq12_eq(const fq12& a, const fq12& b) {
+  const fq2* x = &a.c0.c0;
+  const fq2* y = &b.c0.c0;
+  for (int i = 0; i < 6; i++)
+    if (!fq2_eq(x[i], y[i])) return false;
+  return true;
+}
+}  // namespace
+
+extern "C" {
+// jobs: (proposer j, sender i) pairs.  out[k] = verify_decryption_share result (1/0).
+int cpu_verify_dec_shares(const uint8_t* pk48, uint32_t n, const uint8_t* u48, const uint8_t* v_blob,
+                          const uint64_t* v_off, const uint8_t* w96, const uint8_t* shares48,
+                          const uint32_t* jobs, uint32_t njobs, int threads, uint8_t* out) {
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const uint32_t k = next.fetch_add(1);
+      if (k >= njobs) return;
+      const uint32_t j = jobs[2 * k], i = jobs[2 * k + 1];
+      g1a pk, S, U;
+      g2a W;
+      if (g1_decompress(pk48 + (size_t)i * 48, pk) != HBX_PT_OK || g1_decompress(u48 + (size_t)j * 48, U) != HBX_PT_OK ||
+          g2_decompress(w96 + (size_t)j * 96, W) != HBX_PT_OK ||
+          g1_decompress(shares48 + ((size_t)j * n + i) * 48, S) != HBX_PT_OK) {
+        out[k] = 0;
+        continue;
+      }
+      uint8_t d[32];
+      hash_g1_g2_digest(u48 + (size_t)j * 48, v_blob + v_off[j], v_off[j + 1] - v_off[j], d);
+      chacha_rng r;
+      chacha_rng_from_digest(r, d);
+      const g2a H = g2_to_affine(g2_rand_reference_shape(r));
+      out[k] = fq12_eq(pairing(S, H), pairing(pk, W)) ? 1 : 0;
+    }
+  };
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; t++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return 0;
+}
+}
