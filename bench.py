@@ -51,6 +51,15 @@ MADS_PER_FQMUL = 288
 # Chip peak of 32x32->64-bit integer multiply-add (v_mad_u64_u32), measured by
 # tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
+# HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
+# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_pmc4.sh,
+# profiles/r01_s5_pmc_fq28.txt): 4.289e6 KB + 1.500e7 KB per launch.  The accesses are the
+# kernel's scratch spills (dword / dwordx4 scratch_load/store of the Fq12 state around the
+# out-of-line Fq product), a width the guide leaves uncalibrated, so the raw counter bytes are
+# reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~10 MB
+# (shares 48 B + pk + 26 KB of lines per proposer + 1 B out): the kernel is VALU-bound, and this
+# traffic (~0.6 TB/s at 31 ms) is spill re-reads, not data movement the algorithm needs.
+TRAFFIC_N256_BYTES = (4.289e6 + 1.500e7) * 1024
 
 
 def parse():
@@ -282,7 +291,9 @@ def main():
         "epoch_ms_hip_events": round(float(ms_epoch_ev), 3),
         "kernels_ms": kern,
         "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
-                     "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
+                     "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4),
+                     "traffic": TRAFFIC_N256_BYTES if (n == 256 and pj == 256) else None,
+                     "traffic_note": "bytes/launch, PMC FETCH_SIZE+WRITE_SIZE (scratch spills); algorithmic ~1e7",
                      "kernel": "k_verify_shares", "kernel_ms": ms_kernel,
                      "work": f"{shares_here} shares x {FQMUL_PER_SHARE_VERIFY} Fq-mul x {MADS_PER_FQMUL} MAD"},
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
