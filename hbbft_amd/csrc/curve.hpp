@@ -32,6 +32,7 @@ struct g2j {
 #define HBX_PT_NOT_IN_FIELD 2
 #define HBX_PT_NOT_ON_CURVE 3
 #define HBX_PT_INFINITY 4
+#define HBX_PT_NOT_IN_SUBGROUP 5
 #endif
 
 // ----------------------------------------------------------------------------------------------
@@ -182,6 +183,20 @@ HBX_HD void g1_glv_split(const uint32_t* k8, uint32_t* k1, uint32_t* k2) {
     k1[w] = rem[w];
     k2[w] = q[w];
   }
+}
+
+// P in G1 (the order-r subgroup) for an affine point on the curve -- what pairing 0.14's
+// into_affine checks on deserialisation (is_in_correct_subgroup_assuming_on_curve).
+// Criterion (eprint 2021/1130 sec. 6, proof in 2022/352): phi'(P) == -[x^2] P with
+// phi'(x, y) = (beta^2 x, y).  One 128-bit double-and-add instead of a 255-bit [r] P.
+HBX_HDNI bool g1_is_torsion_free(const g1a& P) {
+  if (P.inf) return true;
+  const g1j m = g1_mul_u128(P, G1_X2);  // [x^2] P
+  if (g1j_is_identity(m)) return false;  // phi'(P) is never O for P != O
+  // (beta^2 x_P, y_P) == -(X/Z^2, Y/Z^3)  <=>  X == beta^2 x_P Z^2  and  Y == -y_P Z^3
+  const fq z2 = fq_sqr(m.z);
+  const fq z3 = fq_mul(z2, m.z);
+  return fq_eq(m.x, fq_mul(fq_mul(P.x, fq_from_const(G1_BETA2)), z2)) && fq_eq(m.y, fq_neg(fq_mul(P.y, z3)));
 }
 
 // zcash compressed G1 -> affine (Montgomery).  No subgroup check.
@@ -374,7 +389,25 @@ HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
   return g2_mul_gls_d(Rp);
 }
 
-// zcash compressed G2 (x.c1 || x.c0) -> affine (Montgomery).  No subgroup check.
+// Jacobian equality (identities included).
+HBX_HD bool g2j_eq(const g2j& a, const g2j& b) {
+  const bool ia = g2j_is_identity(a), ib = g2j_is_identity(b);
+  if (ia || ib) return ia && ib;
+  const fq2 za2 = fq2_sqr(a.z), zb2 = fq2_sqr(b.z);
+  if (!fq2_eq(fq2_mul(a.x, zb2), fq2_mul(b.x, za2))) return false;
+  return fq2_eq(fq2_mul(a.y, fq2_mul(zb2, b.z)), fq2_mul(b.y, fq2_mul(za2, a.z)));
+}
+
+// Q in G2 for an affine point on the twist (pairing's into_affine subgroup check).  Criterion
+// (eprint 2021/1130 sec. 4, proof in 2022/352): psi(Q) == [x] Q -- one 64-bit multiplication.
+HBX_HDNI bool g2_is_torsion_free(const g2a& Q) {
+  if (Q.inf) return true;
+  const g2j q = g2_from_affine(Q);
+  return g2j_eq(g2_neg(g2_mul_u64(q, BLS_X)), g2_psi(q));  // [x] Q with x = -|x|
+}
+
+// zcash compressed G2 (x.c1 || x.c0) -> affine (Montgomery).  No subgroup check here; the
+// ciphertext decode (k_prepare_ct) adds g2_is_torsion_free.
 HBX_HDNI int32_t g2_decompress(const uint8_t* b96, g2a& out) {
   const uint8_t flags = b96[0];
   out.inf = false;

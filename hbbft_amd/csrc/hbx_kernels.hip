@@ -32,6 +32,15 @@ __device__ __forceinline__ bool check2(const line_pre* LA, const g1a& PA, bool q
   const fq12 f = miller_loop2(LA, PA, !skipA, LB, PB, !skipB);
   return fq12_is_one(final_exponentiation(f));
 }
+// check2 with the final exponentiation's base in this lane's LDS slot (pairing.hpp)
+__device__ __forceinline__ bool check2_lds(const line_pre* LA, const g1a& PA, bool qa_inf, const line_pre* LB,
+                                           const g1a& PB, bool qb_inf, lds_u32* gslot) {
+  const bool skipA = PA.inf || qa_inf;
+  const bool skipB = PB.inf || qb_inf;
+  if (skipA && skipB) return true;
+  const fq12 f = miller_loop2(LA, PA, !skipA, LB, PB, !skipB);
+  return fq12_is_one(final_exponentiation_lds(f, gslot));
+}
 
 __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict__ comp, uint32_t n,
                                                       g1a* __restrict__ out, int32_t* __restrict__ status) {
@@ -130,6 +139,7 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                                                       const line_block* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
                                                       uint8_t* __restrict__ valid) {
+  __shared__ uint32_t gslots[144 * LDS_FQ12_STRIDE];  // final-exponentiation base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
@@ -141,7 +151,8 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   if (ok) {
     g1a npk = pk[i];
     npk.y = fq_neg(npk.y);
-    v = check2(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf);
+    v = check2_lds(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf,
+                   (lds_u32*)(gslots + threadIdx.x));
   }
   valid[idx] = v ? 1 : 0;
 }

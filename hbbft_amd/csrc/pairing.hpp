@@ -228,6 +228,71 @@ HBX_HDNI fq12 final_exponentiation(const fq12& f) {
   return fq12_mul(c, t3);
 }
 
+#if defined(__HIPCC__)
+// The same final exponentiation with the exponentiation base parked in LDS.
+// Why: in cyc_exp_abs_x the running power r (144 dwords) and the base g (144 dwords) do not both
+// fit the 256 VGPRs next to the squaring's temporaries, so the compiler spilled ~60 scratch
+// accesses into every cyclotomic squaring and ~560 into every multiplication -- ~300 KB of
+// scratch traffic per share check (profiles/r01_s5_pmc_fq28.txt).  g is read only at the 5 one
+// bits of |x|, so it lives in this lane's LDS slot instead: 144 dwords, lane-interleaved
+// (dword i at base[i * 64]), so a wave's accesses are bank-conflict free.  One slot per lane
+// (36 KB per 64-lane block) keeps the single-wave-per-SIMD occupancy.  Each lane touches only its
+// own slot: no barrier.
+constexpr int LDS_FQ12_STRIDE = 64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void lds_put_fq12(lds_u32* base, const fq12& a) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(&a);
+#pragma unroll
+  for (int i = 0; i < 144; i++) base[i * LDS_FQ12_STRIDE] = p[i];
+}
+__device__ __forceinline__ fq12 lds_get_fq12(const lds_u32* base) {
+  fq12 a;
+  uint32_t* p = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+  for (int i = 0; i < 144; i++) p[i] = base[i * LDS_FQ12_STRIDE];
+  return a;
+}
+// r^(2^k) by k cyclotomic squarings: only r is live in the loop
+__device__ __forceinline__ fq12 cyc_sqr_n(fq12 r, int k) {
+#pragma unroll 1
+  for (int i = 0; i < k; i++) r = fq12_cyclotomic_sqr_i(r);
+  return r;
+}
+// g^|x| with |x| = 0xd201000000010000 written out as runs of squarings between its one bits
+// (bits 63, 62, 60, 57, 48, 16): no per-bit branch, and g is reloaded from LDS only for the five
+// multiplications.
+__device__ __noinline__ fq12 cyc_exp_abs_x_lds(const fq12& g_in, lds_u32* gslot) {
+  static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
+  lds_put_fq12(gslot, g_in);
+  fq12 r = cyc_sqr_n(g_in, 1);  // bit 62
+  r = fq12_mul(r, lds_get_fq12(gslot));
+  r = cyc_sqr_n(r, 2);          // bit 60
+  r = fq12_mul(r, lds_get_fq12(gslot));
+  r = cyc_sqr_n(r, 3);          // bit 57
+  r = fq12_mul(r, lds_get_fq12(gslot));
+  r = cyc_sqr_n(r, 9);          // bit 48
+  r = fq12_mul(r, lds_get_fq12(gslot));
+  r = cyc_sqr_n(r, 32);         // bit 16
+  r = fq12_mul(r, lds_get_fq12(gslot));
+  return cyc_sqr_n(r, 16);      // bits 15..0
+}
+__device__ __forceinline__ fq12 cyc_exp_x_lds(const fq12& g, lds_u32* gslot) {
+  return fq12_conj(cyc_exp_abs_x_lds(g, gslot));
+}
+// f^(3 (p^12 - 1)/r), as final_exponentiation, exponentiations through cyc_exp_x_lds.
+__device__ __noinline__ fq12 final_exponentiation_lds(const fq12& f, lds_u32* gslot) {
+  fq12 t = fq12_mul(fq12_conj(f), fq12_inv(f));
+  t = fq12_mul(fq12_frobenius2(t), t);
+  fq12 a = fq12_mul(cyc_exp_x_lds(t, gslot), fq12_conj(t));
+  a = fq12_mul(cyc_exp_x_lds(a, gslot), fq12_conj(a));
+  fq12 b = fq12_mul(cyc_exp_x_lds(a, gslot), fq12_frobenius(a));
+  fq12 c = fq12_mul(cyc_exp_x_lds(cyc_exp_x_lds(b, gslot), gslot), fq12_frobenius2(b));
+  c = fq12_mul(c, fq12_conj(b));
+  const fq12 t3 = fq12_mul(fq12_cyclotomic_sqr(t), t);
+  return fq12_mul(c, t3);
+}
+#endif
+
 // e(PA, QA) * e(PB, QB) == 1 with prepared lines for QA, QB.
 HBX_HD bool pairing_check2(const line_pre* LA, const g1a& PA, const line_pre* LB, const g1a& PB) {
   const fq12 f = miller_loop2(LA, PA, true, LB, PB, true);

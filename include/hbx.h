@@ -50,6 +50,7 @@ extern "C" {
 #define HBX_PT_NOT_IN_FIELD 2
 #define HBX_PT_NOT_ON_CURVE 3
 #define HBX_PT_INFINITY 4
+#define HBX_PT_NOT_IN_SUBGROUP 5 /* on the curve but not in G1 / G2 (pairing's into_affine rejects it) */
 
 typedef struct hbx_ctx hbx_ctx;
 

@@ -139,3 +139,42 @@ def test_g1_mul_glv(hc):
         out = ctypes.create_string_buffer(48)
         assert hc.hc_g1_mul_glv(comp, _be(k, 32), out) == 0
         assert out.raw == bls.g1_compress(bls.g1_mul(pt, k)), hex(k)
+
+
+def _rand_curve_point_g1(rnd):
+    while True:
+        x = rnd.randrange(bls.P)
+        y = bls.fq_sqrt((x * x * x + bls.B1) % bls.P)
+        if y is not None:
+            return (x, y)
+
+
+def _rand_curve_point_g2(rnd):
+    while True:
+        x = (rnd.randrange(bls.P), rnd.randrange(bls.P))
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is not None:
+            return (x, y)
+
+
+def test_subgroup_checks_match_order_r(hc):
+    """g1_is_torsion_free / g2_is_torsion_free (the endomorphism criteria the ciphertext decode
+    uses) agree with the oracle's [r] P == O on subgroup points and on random curve points, which
+    lie outside G1 / G2 (pairing 0.14's into_affine rejects those)."""
+    rnd = random.Random(23)
+    for k in (1, 5, bls.R - 1, rnd.randrange(1, bls.R)):
+        p1 = bls.g1_mul(bls.G1_GEN, k)
+        assert hc.hc_g1_torsion_free(_be(p1[0]), _be(p1[1])) == 1
+        q = bls.g2_mul(bls.G2_GEN, k)
+        assert hc.hc_g2_torsion_free(_be(q[0][1]) + _be(q[0][0]) + _be(q[1][1]) + _be(q[1][0])) == 1
+    for _ in range(3):
+        p1 = _rand_curve_point_g1(rnd)
+        in_g1 = bls.g1_mul(p1, bls.R) is None
+        assert hc.hc_g1_torsion_free(_be(p1[0]), _be(p1[1])) == int(in_g1)
+        q = _rand_curve_point_g2(rnd)
+        in_g2 = bls.g2_mul(q, bls.R) is None
+        assert hc.hc_g2_torsion_free(_be(q[0][1]) + _be(q[0][0]) + _be(q[1][1]) + _be(q[1][0])) == int(in_g2)
+    # a point of small order times a G1 point: on the curve, not in G1
+    small = bls.g1_mul(_rand_curve_point_g1(rnd), bls.R)  # order divides h1
+    mixed = bls.g1_add(small, bls.g1_mul(bls.G1_GEN, 9))
+    assert hc.hc_g1_torsion_free(_be(mixed[0]), _be(mixed[1])) == 0

@@ -19,6 +19,26 @@ void hc_fq_mul_raw(const uint32_t* a, const uint32_t* b, uint32_t* out) {
   const fq r = fq_mul(x, y);
   for (int i = 0; i < 12; i++) out[i] = r.l[i];
 }
+// subgroup checks on raw affine coordinates (canonical big-endian; G2 as x.c1||x.c0||y.c1||y.c0):
+// 1 = in G1/G2, 0 = not, -1 = not on the curve
+int hc_g1_torsion_free(const uint8_t* x48, const uint8_t* y48) {
+  g1a p;
+  p.x = fq_to_mont(fq_from_be(x48));
+  p.y = fq_to_mont(fq_from_be(y48));
+  p.inf = false;
+  const fq rhs = fq_add(fq_mul(fq_sqr(p.x), p.x), fq_from_const(FQ_B1));
+  if (!fq_eq(fq_sqr(p.y), rhs)) return -1;
+  return g1_is_torsion_free(p) ? 1 : 0;
+}
+int hc_g2_torsion_free(const uint8_t* xy192) {
+  g2a q;
+  q.x = fq2{fq_to_mont(fq_from_be(xy192 + 48)), fq_to_mont(fq_from_be(xy192))};
+  q.y = fq2{fq_to_mont(fq_from_be(xy192 + 144)), fq_to_mont(fq_from_be(xy192 + 96))};
+  q.inf = false;
+  const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(q.x), q.x), g2_b());
+  if (!fq2_eq(fq2_sqr(q.y), rhs)) return -1;
+  return g2_is_torsion_free(q) ? 1 : 0;
+}
 void hc_fq_inv(const uint8_t* a, uint8_t* out) {
   fq x = fq_to_mont(fq_from_be(a));
   fq_to_be(fq_from_mont(fq_inv(x)), out);
