@@ -60,6 +60,9 @@ PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # (shares 48 B + pk + 26 KB of lines per proposer + 1 B out): the kernel is VALU-bound, and this
 # traffic (~0.6 TB/s at 31 ms) is spill re-reads, not data movement the algorithm needs.
 TRAFFIC_N256_BYTES = (4.289e6 + 1.500e7) * 1024
+# The benchmarked node is validator 0: its own decryption shares are computed locally
+# (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
+OWN_INDEX = 0
 
 
 def parse():
@@ -72,6 +75,8 @@ def parse():
     ap.add_argument("--corrupt-every", type=int, default=64)
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-own-share", action="store_true",
+                    help="run Ciphertext::verify as separate checks instead of through the node's own share")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
@@ -99,11 +104,13 @@ def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
     shares = ctx.decrypt_shares(sk_shares, u48)  # (pj + 1, n, 48)
     crng = np.random.default_rng(0x68626278_00000004)
     corrupt = crng.integers(0, corrupt_every, size=(n, n)) == 0  # global (proposer, sender) pattern
+    corrupt[:, OWN_INDEX] = False  # this node's own share is computed locally, never received
     corrupt = corrupt[lo:hi]
     sh = shares[:pj].copy()
     ii = np.nonzero(corrupt)
     sh[ii[0], ii[1]] = shares[pj, ii[1]]
-    return dict(pk_shares=pk_shares, cts=cts[:pj], msgs=msgs[:pj], shares=sh, corrupt=corrupt, t=sks.threshold + 1)
+    return dict(pk_shares=pk_shares, cts=cts[:pj], msgs=msgs[:pj], shares=sh, corrupt=corrupt, t=sks.threshold + 1,
+                own_sk=sk_shares[OWN_INDEX].tobytes())
 
 
 def cpu_baseline(ep, seconds: float, threads: int):
@@ -181,6 +188,8 @@ def main():
     ep = make_epoch(ctx, n, lo, hi, args.vlen, args.corrupt_every)
     st = ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]])
     assert (st == 0).all()
+    if not args.no_own_share:
+        ctx.set_own_share(OWN_INDEX, ep["own_sk"])
 
     # a dedicated stream: torch's default stream is the NULL handle, which the C ABI maps to the
     # context's own stream -- HIP events must be recorded on the stream the kernels run on

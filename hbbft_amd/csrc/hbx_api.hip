@@ -55,6 +55,11 @@ struct hbx_ctx {
   // epoch state
   uint32_t p_ct = 0;
   dbuf U, G2pts, lines, scratch, ct_ok, ct_valid, dec_st;
+  // own-share mode (hbx_set_own_share): this node's index and secret share (8 LE limbs), and its
+  // own decryption shares of the prepared ciphertexts
+  uint32_t own_me = UINT32_MAX;
+  dbuf own_sk, own_S;
+  bool own_ready = false;  // own_S computed by the last prepare
   bool ct_known = false;  // ct_valid computed (else deferred into the next share verification)
   const uint8_t* d_v_blob = nullptr;  // device V blob used by the combine (caller-owned for _d)
   const uint64_t* d_v_off = nullptr;
@@ -344,7 +349,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96};
+                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -371,6 +376,34 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
   return HBX_OK;
 }
 
+int hbx_set_own_share(hbx_ctx* c, uint32_t me, const uint8_t* sk32) {
+  if (!c) return HBX_E_INVALID_ARG;
+  if (!sk32) {  // clear: back to separate Ciphertext::verify checks
+    c->own_me = UINT32_MAX;
+    c->own_ready = false;
+    return HBX_OK;
+  }
+  if (c->n_keys == 0 || me >= c->n_keys) return fail(c, HBX_E_NO_KEYS, "hbx_set_own_share: me=%u, n=%u", me, c->n_keys);
+  static const uint8_t ZERO[32] = {0};
+  if (!scalars_canonical(sk32, 1) || memcmp(sk32, ZERO, 32) == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_own_share: scalar must be in [1, r)");
+  // the secret share must match pk_me: the fused ciphertext check relies on pk_me = sk_me g1
+  uint8_t pk48[48], want[48];
+  int rc = hbx_public_keys(c, sk32, 1, pk48);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy(want, static_cast<uint8_t*>(c->pk_comp.p) + (size_t)me * 48, 48, hipMemcpyDeviceToHost));
+  if (memcmp(pk48, want, 48) != 0) return fail(c, HBX_E_INVALID_ARG, "hbx_set_own_share: sk does not match pk[%u]", me);
+  uint32_t limbs[8];
+  for (int q = 0; q < 8; q++)
+    limbs[q] = ((uint32_t)sk32[31 - 4 * q - 3] << 24) | ((uint32_t)sk32[31 - 4 * q - 2] << 16) |
+               ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
+  if (!c->own_sk.ensure(32)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_own_share: out of device memory");
+  HIPCHK(c, hipMemcpy(c->own_sk.p, limbs, 32, hipMemcpyHostToDevice));
+  c->own_me = me;
+  c->own_ready = false;
+  return HBX_OK;
+}
+
 int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
                               const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
                               uint64_t max_v_len, uint8_t* d_ct_valid, void* stream) {
@@ -388,8 +421,13 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
     timed t_(c, HBX_K_PREPARE_CT, s);
     const uint32_t hash_blocks = (uint32_t)(((size_t)p * HASH_K + 63) / 64);
     const uint32_t dec_blocks = (2 * p + 63) / 64;
+    const bool own = c->own_me != UINT32_MAX;
+    if (own && !c->own_S.ensure((size_t)p * sizeof(g1a)))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
     hipLaunchKernelGGL(k_prepare_ct, dim3(hash_blocks + dec_blocks), b64, 0, s, d_u_comp, d_v_blob, d_v_off,
-                       d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>());
+                       d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
+                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_S.as<g1a>() : nullptr);
+    c->own_ready = own;
   }
   HIPCHK(c, hipGetLastError());
   {
@@ -456,11 +494,15 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
   const size_t m = (size_t)n * p;
   if (!c->S.ensure(m * sizeof(g1a)) || !c->S_status.ensure(m * 4) || !c->valid.ensure(m))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
+  // own-share mode: this node's share is the one computed in prepare, and its check IS
+  // Ciphertext::verify (k_verify_shares); otherwise the ciphertext checks run separately
+  const bool own = c->own_ready && c->own_me < n;
   hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, d_shares, m,
-                     c->S.as<g1a>(), c->S_status.as<int32_t>());
+                     c->S.as<g1a>(), c->S_status.as<int32_t>(), n, own ? c->own_me : UINT32_MAX,
+                     own ? c->own_S.as<g1a>() : nullptr);
   HIPCHK(c, hipGetLastError());
   // ciphertext checks (if prepare deferred them): latency-bound, p checks -> 16-lane groups
-  if (!c->ct_known) {
+  if (!c->ct_known && !own) {
     int rc = launch_pair_checks(c, s, n, p, n, n, d_present);
     if (rc) return rc;
     c->ct_known = true;
@@ -470,9 +512,12 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     timed t_(c, HBX_K_VERIFY_SHARES, s);
     hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
                        c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
-                       c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>());
+                       c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
+                       own ? c->own_me : UINT32_MAX,
+                       (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
   }
   HIPCHK(c, hipGetLastError());
+  c->ct_known = true;
   hipLaunchKernelGGL(k_gate_by_ct, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, c->valid.as<uint8_t>(),
                      c->ct_valid.as<uint8_t>(), n, p);
   HIPCHK(c, hipGetLastError());

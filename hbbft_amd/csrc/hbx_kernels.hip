@@ -67,17 +67,39 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    const uint64_t* __restrict__ v_off,
                                                    const uint8_t* __restrict__ w_comp, uint32_t p,
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
-                                                   g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st) {
+                                                   g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
+                                                   const uint32_t* __restrict__ own_sk, g1a* __restrict__ own_S) {
   if (blockIdx.x >= hash_blocks) {
+    // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2)
     const uint32_t k = (blockIdx.x - hash_blocks) * blockDim.x + threadIdx.x;
     if (k < p) {
       g1a u;
-      dec_st[k] = g1_decompress(u_comp + (size_t)k * 48, u);
+      int32_t st = g1_decompress(u_comp + (size_t)k * 48, u);
+      if (st == HBX_PT_OK && !g1_is_torsion_free(u)) st = HBX_PT_NOT_IN_SUBGROUP;
+      dec_st[k] = st;
       U[k] = u;
+      if (own_sk) {
+        // this node's own decryption share sk_me * U_j (decrypt_share_no_verify,
+        // honey_badger.rs:403), GLV: k = k1 + k2 lambda, phi(x, y) = (beta x, y)
+        g1a sh;
+        sh.x = fq_zero();
+        sh.y = fq_zero();
+        sh.inf = true;
+        if (st == HBX_PT_OK) {
+          uint32_t k1[4], k2[4];
+          g1_glv_split(own_sk, k1, k2);
+          g1a up = u;
+          up.x = fq_mul(up.x, fq_from_const(G1_BETA));
+          sh = g1_to_affine(g1_add(g1_mul_u128(u, k1), g1_mul_u128(up, k2)));
+        }
+        own_S[k] = sh;
+      }
     } else if (k < 2 * p) {
       const uint32_t j = k - p;
       g2a w;
-      dec_st[k] = g2_decompress(w_comp + (size_t)j * 96, w);
+      int32_t st = g2_decompress(w_comp + (size_t)j * 96, w);
+      if (st == HBX_PT_OK && !g2_is_torsion_free(w)) st = HBX_PT_NOT_IN_SUBGROUP;
+      dec_st[k] = st;
       G2pts[2 * j + 1] = w;
     }
     return;
@@ -132,13 +154,20 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
 // with one shared final exponentiation.  At N=256 one epoch is 65,536 independent checks: one
 // lane each keeps every lane of every wave busy with useful work (the throughput-optimal
 // mapping; the 16-lane group executor is kept for the latency-bound per-proposer checks).
+//
+// Own-share mode (me < n, hbx_set_own_share): sender `me` is this node and its share S_j,me =
+// sk_me U_j was computed by k_prepare_ct, not received.  With U_j in G1, W_j and H_j in G2 (the
+// decode checks membership), e(sk U, H) e(-sk g1, W) = (e(U, H) / e(g1, W))^sk and sk != 0 mod r,
+// so that lane's check is exactly Ciphertext::verify (honey_badger.rs:371): its result is also
+// written to ct_valid[j], and the separate 256 ciphertext checks are not needed.
 __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
                                                       const uint8_t* __restrict__ present,
                                                       const g1a* __restrict__ pk, uint32_t n_keys,
                                                       const g2a* __restrict__ G2pts,
                                                       const line_block* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
-                                                      uint8_t* __restrict__ valid) {
+                                                      uint8_t* __restrict__ valid, uint32_t me,
+                                                      uint8_t* __restrict__ ct_valid) {
   __shared__ uint32_t gslots[144 * LDS_FQ12_STRIDE];  // final-exponentiation base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
@@ -146,7 +175,7 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   const size_t idx = (size_t)j * n + i;
   const int32_t st = s_status[idx];
   const bool ok = (st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && ct_ok[j] &&
-                  (present == nullptr || present[idx]);
+                  (present == nullptr || present[idx] || i == me);
   bool v = false;
   if (ok) {
     g1a npk = pk[i];
@@ -155,6 +184,7 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                    (lds_u32*)(gslots + threadIdx.x));
   }
   valid[idx] = v ? 1 : 0;
+  if (i == me && ct_valid) ct_valid[j] = v ? 1 : 0;
 }
 
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
@@ -445,12 +475,24 @@ __global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
 }
 
 // One lane per share: decompress S_ji (kept for the verification and the Lagrange combine).
+// Decode = pairing 0.14's into_affine (on-curve and G1 membership), as the reference deserialises
+// a DecryptionShare.  In own-share mode the entry of sender `me` is this node's own share from
+// k_prepare_ct instead of the received bytes.
 __global__ void __launch_bounds__(256) k_decompress_shares(const uint8_t* __restrict__ shares, size_t count,
-                                                           g1a* __restrict__ S, int32_t* __restrict__ status) {
+                                                           g1a* __restrict__ S, int32_t* __restrict__ status,
+                                                           uint32_t n, uint32_t me, const g1a* __restrict__ own_S) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
+  if (own_S && (uint32_t)(i % n) == me) {
+    const g1a o = own_S[i / n];
+    S[i] = o;
+    status[i] = o.inf ? HBX_PT_INFINITY : HBX_PT_OK;
+    return;
+  }
   g1a p;
-  status[i] = g1_decompress(shares + i * 48, p);
+  int32_t st = g1_decompress(shares + i * 48, p);
+  if (st == HBX_PT_OK && !g1_is_torsion_free(p)) st = HBX_PT_NOT_IN_SUBGROUP;
+  status[i] = st;
   S[i] = p;
 }
 

@@ -35,6 +35,7 @@ EXPORTS = (
     "hbx_last_error",
     "hbx_version",
     "hbx_set_pk_shares",
+    "hbx_set_own_share",
     "hbx_prepare_ciphertexts",
     "hbx_verify_dec_shares",
     "hbx_combine_decrypt",
@@ -91,6 +92,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_last_error.restype = ctypes.c_char_p
     lib.hbx_version.restype = ctypes.c_char_p
     lib.hbx_set_pk_shares.argtypes = [P, u8p, u32, i32p]
+    lib.hbx_set_own_share.argtypes = [P, u32, u8p]
     lib.hbx_prepare_ciphertexts.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
     lib.hbx_verify_dec_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
     lib.hbx_combine_decrypt.argtypes = [P, u32, u8p, i32p]
@@ -251,6 +253,15 @@ class Context:
         out = np.zeros((p, n, 48), dtype=np.uint8)
         self._check(self.lib.hbx_decrypt_shares(self.h, _u8(sk32), n, _u8(u48), p, _u8(out)))
         return out
+
+    def set_own_share(self, me: int, sk32=None):
+        """hbx_set_own_share: this node's index and 32-byte big-endian secret share (None clears)."""
+        if sk32 is None:
+            self._check(self.lib.hbx_set_own_share(self.h, 0, None))
+            return
+        sk = np.frombuffer(bytes(sk32), dtype=np.uint8).copy()
+        assert sk.size == 32
+        self._check(self.lib.hbx_set_own_share(self.h, me, _u8(sk)))
 
     # -- device API (torch tensors as HBM buffers; torch is plumbing only) -----------------------
     def prepare_ciphertexts_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_ct_valid=None, stream=None):

@@ -91,6 +91,20 @@ int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launch
 int hbx_set_pk_shares(hbx_ctx* ctx, const uint8_t* pk_comp, uint32_t n, int32_t* status);
 
 /* ---------------------------------------------------------------------------------------------
+ * This node's own secret key share (once per era; optional).
+ * Replaces: the node's own share path -- SecretKeyShare::decrypt_share_no_verify in
+ * send_decryption_share (src/honey_badger/honey_badger.rs:394-418), whose result the node feeds
+ * back to itself as sender `me`.  With it set, hbx_prepare_ciphertexts* computes S_j,me = sk_me U_j
+ * for every ciphertext, hbx_verify_dec_shares* uses it for sender `me` (that row of the share
+ * input is ignored), and the check of that share doubles as Ciphertext::verify (:371): U_j, W_j are
+ * decoded with subgroup checks and H_j is in G2, so e(sk U, H) e(-sk g1, W) = 1 exactly when
+ * e(U, H) = e(g1, W) (sk != 0 mod r).  This removes the separate latency-bound ciphertext checks.
+ * sk32: canonical big-endian scalar in [1, r) matching pk[me] of hbx_set_pk_shares
+ * (HBX_E_INVALID_ARG otherwise); NULL clears the mode.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_set_own_share(hbx_ctx* ctx, uint32_t me, const uint8_t* sk32);
+
+/* ---------------------------------------------------------------------------------------------
  * Ciphertexts of one epoch (one per accepted proposer).
  * Replaces: threshold_crypto Ciphertext::verify (src/honey_badger/honey_badger.rs:371) and
  * hoists hash_g1_g2(U_j, V_j) -- recomputed by the reference inside every

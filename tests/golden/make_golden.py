@@ -117,6 +117,30 @@ def make_epoch(n: int):
     for j in range(p):
         if status[j] == 0:
             plain_blob[int(v_off[j]):int(v_off[j + 1])] = np.frombuffer(plains[j], dtype=np.uint8)
+
+    # Own-share mode (hbx_set_own_share): node `me` uses its own share sk_me * U_j
+    # (decrypt_share_no_verify, honey_badger.rs:403) whatever its row of the input holds; that
+    # honest share verifies exactly when the ciphertext does.
+    me = n - 2
+    own_pts = dict(share_pts)
+    for j in range(p):
+        own_pts[(j, me)] = tc.decrypt_share(sk_shares[me], bad_cts[j])
+    expect_valid_own = expect_valid.copy()
+    for j in range(p):
+        expect_valid_own[j, me] = bool(ct_valid[j])
+    status_own = np.zeros(p, dtype=np.int32)
+    plain_blob_own = np.zeros(int(v_off[-1]), dtype=np.uint8)
+    for j in range(p):
+        if not ct_valid[j]:
+            status_own[j] = -7
+            continue
+        idx = [i for i in range(n) if expect_valid_own[j, i]]
+        if len(idx) < t:
+            status_own[j] = -3
+            continue
+        pt = tc.decrypt(pks, [(i, own_pts[(j, i)]) for i in idx], bad_cts[j])
+        assert pt == msgs[j]
+        plain_blob_own[int(v_off[j]):int(v_off[j + 1])] = np.frombuffer(pt, dtype=np.uint8)
     return dict(
         n=np.int64(n), t=np.int64(t),
         pk_comp=np.stack([np.frombuffer(bls.g1_compress(q), dtype=np.uint8) for q in pk_shares]),
@@ -131,6 +155,11 @@ def make_epoch(n: int):
         expect_valid=expect_valid,
         expect_status=status,
         expect_plain_blob=plain_blob,
+        own_me=np.int64(me),
+        own_sk=np.frombuffer(sk_shares[me].to_bytes(32, "big"), dtype=np.uint8),
+        expect_valid_own=expect_valid_own,
+        expect_status_own=status_own,
+        expect_plain_blob_own=plain_blob_own,
     )
 
 

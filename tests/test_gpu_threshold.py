@@ -71,3 +71,50 @@ def test_fused_epoch_call_matches_golden(hbx_ctx, n):
     for j in range(p):
         if status[j] == 0:
             assert out[off[j]:off[j + 1]].tobytes() == d["expect_plain_blob"][int(off[j]):int(off[j + 1])].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 7])
+def test_own_share_mode_matches_golden(hbx_ctx, n):
+    """hbx_set_own_share: node `me`'s own share replaces its input row, and that share's check is
+    Ciphertext::verify (no separate ciphertext checks).  The fixture's own-mode expectations come
+    from the oracle (tests/golden/make_golden.py): the invalid ciphertext is still caught, and the
+    starved proposer gains our honest share."""
+    d = _load(n)
+    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
+    me = int(d["own_me"])
+    hbx_ctx.set_own_share(me, d["own_sk"].tobytes())
+    try:
+        ct_ok = hbx_ctx.prepare_ciphertexts(_cts(d))  # immediate Ciphertext::verify (wide path)
+        np.testing.assert_array_equal(ct_ok, d["expect_ct_valid"])
+        valid = hbx_ctx.verify_dec_shares(d["shares"], d["present"])
+        np.testing.assert_array_equal(valid, d["expect_valid_own"])
+        plains, status = hbx_ctx.combine_decrypt(int(d["t"]))
+        np.testing.assert_array_equal(status, d["expect_status_own"])
+        off = d["v_off"]
+        for j, pt in enumerate(plains):
+            if status[j] == 0:
+                assert pt == d["expect_plain_blob_own"][int(off[j]):int(off[j + 1])].tobytes()
+        # deferred ciphertext checks: the own share's lane decides ct validity
+        import torch
+
+        dev = torch.device("cuda", 0)
+        p = len(off) - 1
+        t_u = torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev)
+        t_w = torch.from_numpy(np.ascontiguousarray(d["w"])).to(dev)
+        t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"]).copy()).to(dev)
+        t_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+        t_sh = torch.from_numpy(np.ascontiguousarray(d["shares"])).to(dev)
+        t_pr = torch.from_numpy(np.ascontiguousarray(d["present"]).astype(np.uint8)).to(dev)
+        t_out = torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
+        t_valid = torch.zeros(p * n, dtype=torch.uint8, device=dev)
+        t_ct = torch.zeros(p, dtype=torch.uint8, device=dev)
+        t_st = torch.zeros(p, dtype=torch.int32, device=dev)
+        hbx_ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, p, int(np.max(np.diff(off))), t_sh, n, int(d["t"]), t_out,
+                                d_valid=t_valid, d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(t_ct.cpu().numpy(), d["expect_ct_valid"])
+        np.testing.assert_array_equal(t_valid.cpu().numpy().reshape(p, n), d["expect_valid_own"])
+        np.testing.assert_array_equal(t_st.cpu().numpy(), d["expect_status_own"])
+    finally:
+        hbx_ctx.set_own_share(me, None)
