@@ -53,13 +53,13 @@ MADS_PER_FQMUL = 288
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
 # rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_pmc4.sh,
-# profiles/r01_s5_pmc_fq28.txt): 4.289e6 KB + 1.500e7 KB per launch.  The accesses are the
+# profiles/r01_s6_pmc_n256.txt): 3.232e6 KB + 6.434e6 KB per launch.  The accesses are the
 # kernel's scratch spills (dword / dwordx4 scratch_load/store of the Fq12 state around the
 # out-of-line Fq product), a width the guide leaves uncalibrated, so the raw counter bytes are
 # reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~10 MB
 # (shares 48 B + pk + 26 KB of lines per proposer + 1 B out): the kernel is VALU-bound, and this
-# traffic (~0.6 TB/s at 31 ms) is spill re-reads, not data movement the algorithm needs.
-TRAFFIC_N256_BYTES = (4.289e6 + 1.500e7) * 1024
+# traffic (~0.32 TB/s at 30.7 ms) is spill re-reads, not data movement the algorithm needs.
+TRAFFIC_N256_BYTES = (3.232e6 + 6.434e6) * 1024
 # The benchmarked node is validator 0: its own decryption shares are computed locally
 # (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
 OWN_INDEX = 0

@@ -115,7 +115,8 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
 }
 
-// One lane per G2 point: the 68 normalised lines.  With `dec_st` (ciphertext points), lane 2j also
+// One lane per G2 point: the 68 raw lines (c2 into `scratch`, count x 68 Fq2), normalised by
+// k_normalise_lines.  With `dec_st` (ciphertext points), lane 2j also
 // settles ct_ok[j]: U_j and W_j must decode (threshold_crypto deserialisation); otherwise H_j is
 // replaced by the identity and the proposer's checks are gated off.
 __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
@@ -143,10 +144,24 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
     for (int i = 0; i < MILLER_LINES; i++) {
       lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
       lines[(size_t)k * MILLER_LINES + i].c1 = fq2_zero();
+      scratch[(size_t)k * MILLER_LINES + i] = fq2_one();
     }
     return;
   }
-  g2_prepare_lines(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * 2 * MILLER_LINES);
+  g2_raw_lines(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES);
+}
+
+// Second half of the line preparation: one lane per raw line, (c0, c1) /= c2.  68 independent
+// Fq2 inversions replace the batched inversion (3 x 68 Fq2 products plus one inversion) that
+// used to sit at the end of each point's sequential chain: the chain of k_prepare_lines is the
+// 68 T steps only, and this launch is 68x wider and one inversion deep.
+__global__ void __launch_bounds__(64) k_normalise_lines(line_pre* __restrict__ lines,
+                                                        const fq2* __restrict__ c2, uint32_t count) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  line_pre l = lines[k];
+  g2_normalise_line(l, c2[k]);
+  lines[k] = l;
 }
 
 // Share verification, one lane per share (lane = sender i, blockIdx.y = proposer j):

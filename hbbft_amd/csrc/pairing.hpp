@@ -83,36 +83,45 @@ HBX_HDNI void line_add_step(g2j& T, const g2a& Q, fq2& c0, fq2& c1, fq2& c2) {
   T = g2j{X3, Y3, Z3};
 }
 
-// Prepare the 68 normalised lines of Q (affine, not infinity).  `scratch` holds 2*68 Fq2 of
-// per-lane workspace (raw c2 values and their prefix products for one batched inversion).
-HBX_HDNI void g2_prepare_lines(const g2a& Q, line_pre* out, fq2* scratch) {
+// The 68 raw lines of Q (affine, not infinity): out[k] = (c0, c1) and c2[k] = the y_P
+// coefficient, in loop order.  Only the T chain is sequential; normalising (c0, c1) / c2 is 68
+// independent inversions (g2_normalise_line), so the device does them one lane per line
+// (k_normalise_lines) instead of a batched inversion at the end of this lane's chain.
+HBX_HDNI void g2_raw_lines(const g2a& Q, line_pre* out, fq2* c2) {
   g2j T = g2_from_affine(Q);
-  fq2 pp = fq2_one();
   int k = 0;
   for (int i = 62; i >= 0; i--) {
-    fq2 c0, c1, c2;
-    line_dbl_step(T, c0, c1, c2);
-    out[k].c0 = c0;
-    out[k].c1 = c1;
-    pp = fq2_mul(pp, c2);
-    scratch[2 * k] = c2;
-    scratch[2 * k + 1] = pp;
+    line_dbl_step(T, out[k].c0, out[k].c1, c2[k]);
     k++;
     if ((BLS_X >> i) & 1) {
-      line_add_step(T, Q, c0, c1, c2);
-      out[k].c0 = c0;
-      out[k].c1 = c1;
-      pp = fq2_mul(pp, c2);
-      scratch[2 * k] = c2;
-      scratch[2 * k + 1] = pp;
+      line_add_step(T, Q, out[k].c0, out[k].c1, c2[k]);
       k++;
     }
   }
+}
+
+// One line scaled so its y_P coefficient is 1.
+HBX_HD void g2_normalise_line(line_pre& l, const fq2& c2) {
+  const fq2 inv = fq2_inv(c2);
+  l.c0 = fq2_mul(l.c0, inv);
+  l.c1 = fq2_mul(l.c1, inv);
+}
+
+// Prepare the 68 normalised lines of Q (affine, not infinity) in one lane (host tools).
+// `scratch` holds 2*68 Fq2 of workspace (raw c2 values and their prefix products for one
+// batched inversion).
+HBX_HDNI void g2_prepare_lines(const g2a& Q, line_pre* out, fq2* scratch) {
+  g2_raw_lines(Q, out, scratch);
+  fq2 pp = fq2_one();
+  for (int k = 0; k < MILLER_LINES; k++) {
+    pp = fq2_mul(pp, scratch[k]);
+    scratch[MILLER_LINES + k] = pp;
+  }
   fq2 inv = fq2_inv(pp);
   for (int j = MILLER_LINES - 1; j >= 0; j--) {
-    const fq2 prev = j > 0 ? scratch[2 * (j - 1) + 1] : fq2_one();
+    const fq2 prev = j > 0 ? scratch[MILLER_LINES + j - 1] : fq2_one();
     const fq2 c2inv = fq2_mul(inv, prev);
-    inv = fq2_mul(inv, scratch[2 * j]);
+    inv = fq2_mul(inv, scratch[j]);
     out[j].c0 = fq2_mul(out[j].c0, c2inv);
     out[j].c1 = fq2_mul(out[j].c1, c2inv);
   }
