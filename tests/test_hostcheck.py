@@ -43,6 +43,28 @@ def test_fq_mul_inv(hc):
         assert int.from_bytes(out.raw, "big") * a % bls.P == 1
 
 
+def _limbs(x, n):
+    return (ctypes.c_uint32 * n)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(n)])
+
+
+def test_binary_inversion_montgomery(hc):
+    """fq_inv / fr_inv (binary extended Euclid + R^3 fix-up): Montgomery in, Montgomery out,
+    for canonical and lazy-range (x + p) operands, the extremes, and 0 -> 0 (as x^(m-2))."""
+    rnd = random.Random(11)
+    for mod, n, bits, fn in ((bls.P, 12, 384, hc.hc_fq_inv_raw), (bls.R, 8, 256, hc.hc_fr_inv_raw)):
+        R = 1 << bits
+        xs = [0, 1, 2, mod - 1, mod - 2, (mod - 1) // 2] + [rnd.randrange(mod) for _ in range(200)]
+        for x in xs:
+            m = x * R % mod
+            reps = [m] + ([m + mod] if mod == bls.P and m + mod < 2 * mod else [])
+            for rep in reps:
+                out = (ctypes.c_uint32 * n)()
+                fn(_limbs(rep, n), out)
+                got = sum(int(out[i]) << (32 * i) for i in range(n))
+                want = 0 if x == 0 else pow(x, -1, mod) * R % mod
+                assert got == want, (hex(x), hex(rep))
+
+
 def test_fq_mul_lazy_range(hc):
     """The digit-sliced Montgomery product on lazy operands in [0, 2p]: r = a b / 2^384 mod p and
     r < 2p (the bound the tower relies on), including the extremes 0, p, 2p - 1 and 2p."""

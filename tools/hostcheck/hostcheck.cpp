@@ -43,6 +43,19 @@ void hc_fq_inv(const uint8_t* a, uint8_t* out) {
   fq x = fq_to_mont(fq_from_be(a));
   fq_to_be(fq_from_mont(fq_inv(x)), out);
 }
+// raw Montgomery limbs (lazy range allowed): fq_inv / fr_inv themselves
+void hc_fq_inv_raw(const uint32_t* a, uint32_t* out) {
+  fq x;
+  for (int i = 0; i < 12; i++) x.l[i] = a[i];
+  const fq r = fq_canon(fq_inv(x));
+  for (int i = 0; i < 12; i++) out[i] = r.l[i];
+}
+void hc_fr_inv_raw(const uint32_t* a, uint32_t* out) {
+  fr x;
+  for (int i = 0; i < 8; i++) x.l[i] = a[i];
+  const fr r = fr_csub(fr_inv(x));
+  for (int i = 0; i < 8; i++) out[i] = r.l[i];
+}
 int hc_g1_roundtrip(const uint8_t* in48, uint8_t* out48) {
   g1a p; int st = g1_decompress(in48, p);
   if (st != HBX_PT_OK && st != HBX_PT_INFINITY) return st;
