@@ -154,6 +154,26 @@ HBX_HDNI g1j g1_mul_u128(const g1a& P, const uint32_t* k4) {
   return acc;
 }
 
+// Same product with a fixed 4-bit window, for scalars that differ across the lanes of a wave
+// (the Lagrange combine): double-and-add issues the addition whenever ANY lane has a 1 bit,
+// i.e. ~128 mixed additions per wave, while here every lane adds its own table entry once per
+// window: 124 doublings + 31 additions + 14 table additions.  The table (0..15) P sits in
+// per-lane scratch (dynamically indexed); a zero digit takes g1_add's identity early-out.
+HBX_HDNI g1j g1_mul_u128_w4(const g1a& P, const uint32_t* k4) {
+  g1j tab[16];
+  tab[0] = g1_identity();
+  tab[1] = g1_from_affine(P);
+#pragma unroll 1
+  for (int i = 2; i < 16; i++) tab[i] = g1_add_mixed_i(tab[i - 1], P);
+  g1j acc = tab[k4[3] >> 28];
+#pragma unroll 1
+  for (int w = 30; w >= 0; w--) {
+    acc = g1_dbl(g1_dbl(g1_dbl(g1_dbl(acc))));
+    acc = g1_add(acc, tab[(k4[w >> 3] >> ((w & 7) * 4)) & 0xFu]);
+  }
+  return acc;
+}
+
 // GLV split of a canonical scalar k < r: k = k1 + k2 lambda with lambda = x^2 - 1 (128 bits),
 // k1 = k mod lambda, k2 = k div lambda (< lambda + 2 < 2^128 since r = lambda^2 + lambda + 1).
 // Then k P = k1 P + k2 phi(P), phi(x, y) = (beta x, y).

@@ -103,7 +103,7 @@ int hc_g1_mul_glv(const uint8_t* in48, const uint8_t* k32, uint8_t* out48) {
   g1_glv_split(k8, k1, k2);
   g1a ph = p;
   ph.x = fq_mul(p.x, fq_from_const(G1_BETA));
-  g1j r = g1_add(g1_mul_u128(p, k1), g1_mul_u128(ph, k2));
+  g1j r = g1_add(g1_mul_u128_w4(p, k1), g1_mul_u128_w4(ph, k2));  // k_combine's windowed product
   g1_compress(g1_to_affine(r), out48); return 0;
 }
 int hc_g2_clear_cofactor(const uint8_t* in96, uint8_t* out96) {
