@@ -209,6 +209,104 @@ HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
 }
 
 #if defined(__HIPCC__)
+// ---- group-cooperative G2 doubling for the cofactor clearing --------------------------------
+// The cofactor clearing is ~200 sequential doublings on one point: a latency chain, run by one
+// lane per proposer while the other lanes of its hash group idle.  Here the 8 lanes of the group
+// (all holding the same point) split each doubling's 16 Fq products into three rounds of
+// independent products, one per lane, exchanged through ds_bpermute (__shfl).  Same formulas
+// as g2_dbl (dbl-2009-l); Fq2 products by schoolbook (four Fq products on four lanes), so the
+// coordinates are equal mod p to g2_dbl's.  Control flow must be group-uniform.
+__device__ __forceinline__ fq fq_from_lane(const fq& v, int src) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__shfl((int)v.l[i], src, 64);
+  return r;
+}
+__device__ __forceinline__ fq fq_sel8(int s, const fq& v0, const fq& v1, const fq& v2, const fq& v3, const fq& v4,
+                                      const fq& v5, const fq& v6, const fq& v7) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t lo = (s & 2) ? ((s & 1) ? v3.l[i] : v2.l[i]) : ((s & 1) ? v1.l[i] : v0.l[i]);
+    const uint32_t hi = (s & 2) ? ((s & 1) ? v7.l[i] : v6.l[i]) : ((s & 1) ? v5.l[i] : v4.l[i]);
+    r.l[i] = (s & 4) ? hi : lo;
+  }
+  return r;
+}
+__device__ __noinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
+  const int s = gl & 7;
+  const fq x0 = p.x.c0, x1 = p.x.c1, y0 = p.y.c0, y1 = p.y.c1, z0 = p.z.c0, z1 = p.z.c1;
+  // round 1: A = X^2 (lanes 0, 1), B = Y^2 (2, 3), Y Z (4..7)
+  fq r = fq_mul(fq_sel8(s, fq_add(x0, x1), x0, fq_add(y0, y1), y0, y0, y1, y0, y1),
+                fq_sel8(s, fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, z0, z1, z1, z0));
+  const fq2 A = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
+  const fq2 B = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
+  const fq2 YZ = fq2{fq_sub(fq_from_lane(r, gbase + 4), fq_from_lane(r, gbase + 5)),
+                     fq_add(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7))};
+  // round 2: C = B^2 (0, 1), T = (X + B)^2 (2, 3), F = E^2 with E = 3A (4, 5)
+  const fq2 S = fq2_add(p.x, B);
+  const fq2 E = fq2_add(fq2_dbl(A), A);
+  r = fq_mul(fq_sel8(s, fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0, E.c0, E.c0),
+             fq_sel8(s, fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1, E.c1, E.c1));
+  const fq2 C = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
+  const fq2 T = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
+  const fq2 F = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
+  const fq2 D = fq2_dbl(fq2_sub(fq2_sub(T, A), C));
+  const fq2 X3 = fq2_sub(F, fq2_dbl(D));
+  // round 3: E (D - X3) (0..3)
+  const fq2 G = fq2_sub(D, X3);
+  r = fq_mul(fq_sel8(s, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1),
+             fq_sel8(s, G.c0, G.c1, G.c1, G.c0, G.c0, G.c1, G.c1, G.c0));
+  const fq2 EG = fq2{fq_sub(fq_from_lane(r, gbase + 0), fq_from_lane(r, gbase + 1)),
+                     fq_add(fq_from_lane(r, gbase + 2), fq_from_lane(r, gbase + 3))};
+  const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
+  return g2j{X3, fq2_sub(EG, C8), fq2_dbl(YZ)};
+}
+__device__ __forceinline__ g2j g2_dbl_n_group(g2j p, int n, int gl, int gbase) {
+  for (int i = 0; i < n; i++) p = g2_dbl_group(p, gl, gbase);
+  return p;
+}
+// g2_mul_u64 / g2_mul_gls_d / g2_clear_cofactor (curve.hpp) with the group doubling
+__device__ g2j g2_mul_u64_group(const g2j& p, uint64_t k, int gl, int gbase) {
+  g2j acc = p;
+  const int top = 63 - __builtin_clzll(k);
+  for (int i = top - 1; i >= 0; i--) {
+    acc = g2_dbl_group(acc, gl, gbase);
+    if ((k >> i) & 1) acc = g2_add(acc, p);
+  }
+  return acc;
+}
+__device__ g2j g2_mul_gls_d_group(const g2j& P, int gl, int gbase) {
+  const g2j P2 = g2_dbl_group(P, gl, gbase);
+  const g2j P4 = g2_dbl_group(P2, gl, gbase);
+  g2j Z = g2_add(P4, P);
+  Z = g2_add(g2_dbl_n_group(Z, 4, gl, gbase), Z);
+  Z = g2_add(g2_dbl_n_group(Z, 8, gl, gbase), Z);
+  const g2j W = g2_add(g2_dbl_group(Z, gl, gbase), P);
+  g2j acc = g2_add(g2_dbl_n_group(P2, 3, gl, gbase), P);
+  acc = g2_add(g2_dbl_group(acc, gl, gbase), P);
+  acc = g2_dbl_n_group(acc, 1 + 8 + 16, gl, gbase);
+  acc = g2_add(acc, Z);
+  acc = g2_add(g2_dbl_n_group(acc, 16, gl, gbase), Z);
+  return g2_add(g2_dbl_n_group(acc, 16, gl, gbase), W);
+}
+__device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
+  const g2j t1 = g2_neg(g2_mul_u64_group(P, BLS_X, gl, gbase));
+  g2j t2 = g2_psi(P);
+  g2j t3 = g2_psi(g2_psi(g2_dbl_group(P, gl, gbase)));
+  t3 = g2_sub(t3, t2);
+  t2 = g2_add(t1, t2);
+  t2 = g2_neg(g2_mul_u64_group(t2, BLS_X, gl, gbase));
+  t3 = g2_add(t3, t2);
+  t3 = g2_sub(t3, t1);
+  const g2j Q = g2_sub(t3, P);
+  const g2j q1 = g2_psi(Q);
+  const g2j q2 = g2_psi(q1);
+  const g2j q3 = g2_psi(q2);
+  const g2j Rp = g2_sub(g2_sub(g2_add(Q, q1), q2), q3);
+  return g2_mul_gls_d_group(Rp, gl, gbase);
+}
+
 // hash_g2 by a GROUP of K aligned lanes of one wave (K | 64), same point as g2_rand_from_rng.
 //
 // Why.  One lane per hash leaves a wave waiting for its unluckiest lane: every lane draws
@@ -222,7 +320,7 @@ HBX_HDNI g2j g2_rand_from_rng(chacha_rng& r) {
 // Returns true on the lane that holds the result in `out`.
 template <int K>
 __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
-  static_assert(K >= 2 && K <= 32 && (64 % K) == 0, "group size");
+  static_assert(K >= 8 && K <= 32 && (64 % K) == 0, "group size (the cofactor clearing uses 8 lanes)");
   if (!active) return false;
   const int lane = (int)(threadIdx.x & 63);
   const int gl = lane % K;
@@ -255,14 +353,18 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
       continue;
     }
     const int win = __builtin_ctzll(pass) - gbase;
-    bool ident = false;
+    fq2 y = fq2_zero();
     if (gl == win) {
-      fq2 y = c1zero ? y0 : fq2_sqrt_from_norm(rhs, s);
+      y = c1zero ? y0 : fq2_sqrt_from_norm(rhs, s);
       // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
       if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
-      out = g2_clear_cofactor(g2j{x, y, fq2_one()});
-      ident = g2j_is_identity(out);
     }
+    // the winner's point to every lane of the group, then the cooperative cofactor clearing
+    const int src = gbase + win;
+    const fq2 xw = fq2{fq_from_lane(x.c0, src), fq_from_lane(x.c1, src)};
+    const fq2 yw = fq2{fq_from_lane(y.c0, src), fq_from_lane(y.c1, src)};
+    out = g2_clear_cofactor_group(g2j{xw, yw, fq2_one()}, gl, gbase);
+    const bool ident = g2j_is_identity(out);
     if ((__ballot(ident) & gmask) == 0) return gl == win;
     base += (uint32_t)win + 1;
   }
