@@ -432,7 +432,7 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
+    hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p * LINE_K + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>());
     HIPCHK(c, hipGetLastError());
@@ -651,7 +651,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+    hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
                        c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;

@@ -115,40 +115,143 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
 }
 
-// One lane per G2 point: the 68 raw lines (c2 into `scratch`, count x 68 Fq2), normalised by
-// k_normalise_lines.  With `dec_st` (ciphertext points), lane 2j also
+// Lanes per G2 point in k_prepare_lines.
+constexpr int LINE_K = 16;
+
+__device__ __forceinline__ fq fq_sel16(int s, const fq (&v)[16]) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint32_t t = v[0].l[i];
+#pragma unroll
+    for (int k = 1; k < 16; k++) t = (s == k) ? v[k].l[i] : t;
+    r.l[i] = t;
+  }
+  return r;
+}
+
+// line_dbl_step (pairing.hpp) on the LINE_K lanes of a group that all hold T: its 26 Fq
+// products as three rounds of independent products, one per lane (10, 14 and 8 lanes busy),
+// exchanged by ds_bpermute; Fq2 products by schoolbook.  Same values mod p as line_dbl_step.
+__device__ __noinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& c2, int gl, int gbase) {
+  const fq x0 = T.x.c0, x1 = T.x.c1, y0 = T.y.c0, y1 = T.y.c1, z0 = T.z.c0, z1 = T.z.c1;
+  // round 1: A = X^2 (0, 1), B = Y^2 (2, 3), ZZ = Z^2 (4, 5), Y Z (6..9)
+  fq r;
+  {
+    const fq a[16] = {fq_add(x0, x1), x0, fq_add(y0, y1), y0, fq_add(z0, z1), z0, y0, y1, y0, y1,
+                      x0, x0, x0, x0, x0, x0};
+    const fq b[16] = {fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, fq_sub(z0, z1), z1, z0, z1, z1, z0,
+                      x1, x1, x1, x1, x1, x1};
+    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+  }
+  const fq2 A = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
+  const fq2 B = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
+  const fq2 ZZ = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
+  const fq2 YZ = fq2{fq_sub(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7)),
+                     fq_add(fq_from_lane(r, gbase + 8), fq_from_lane(r, gbase + 9))};
+  // round 2: C = B^2 (0, 1), (X + B)^2 (2, 3), F = E^2 (4, 5), E X (6..9), E ZZ (10..13)
+  const fq2 E = fq2_add(fq2_dbl(A), A);
+  const fq2 S = fq2_add(T.x, B);
+  {
+    const fq a[16] = {fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0,
+                      E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c0};
+    const fq b[16] = {fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1,
+                      x0, x1, x1, x0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0, E.c1, E.c1};
+    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+  }
+  const fq2 C = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
+  const fq2 TT = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
+  const fq2 F = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
+  const fq2 EX = fq2{fq_sub(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7)),
+                     fq_add(fq_from_lane(r, gbase + 8), fq_from_lane(r, gbase + 9))};
+  const fq2 EZZ = fq2{fq_sub(fq_from_lane(r, gbase + 10), fq_from_lane(r, gbase + 11)),
+                      fq_add(fq_from_lane(r, gbase + 12), fq_from_lane(r, gbase + 13))};
+  c0 = fq2_sub(EX, fq2_dbl(B));
+  c1 = fq2_neg(EZZ);
+  const fq2 D = fq2_dbl(fq2_sub(fq2_sub(TT, A), C));
+  const fq2 X3 = fq2_sub(F, fq2_dbl(D));
+  const fq2 Z3 = fq2_dbl(YZ);
+  // round 3: E (D - X3) (0..3), c2 = Z3 ZZ (4..7)
+  const fq2 G = fq2_sub(D, X3);
+  {
+    const fq a[16] = {E.c0, E.c1, E.c0, E.c1, Z3.c0, Z3.c1, Z3.c0, Z3.c1,
+                      E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0};
+    const fq b[16] = {G.c0, G.c1, G.c1, G.c0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0,
+                      G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0};
+    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+  }
+  const fq2 EG = fq2{fq_sub(fq_from_lane(r, gbase + 0), fq_from_lane(r, gbase + 1)),
+                     fq_add(fq_from_lane(r, gbase + 2), fq_from_lane(r, gbase + 3))};
+  c2 = fq2{fq_sub(fq_from_lane(r, gbase + 4), fq_from_lane(r, gbase + 5)),
+           fq_add(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7))};
+  const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
+  T = g2j{X3, fq2_sub(EG, C8), Z3};
+}
+
+// g2_raw_lines on a lane group; group lane 0 writes the lines.
+__device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int gl, int gbase) {
+  g2j T = g2_from_affine(Q);
+  int k = 0;
+  for (int i = 62; i >= 0; i--) {
+    fq2 c0, c1, c2;
+    line_dbl_step_group(T, c0, c1, c2, gl, gbase);
+    if (gl == 0) {
+      out[k].c0 = c0;
+      out[k].c1 = c1;
+      c2out[k] = c2;
+    }
+    k++;
+    if ((BLS_X >> i) & 1) {
+      line_add_step(T, Q, c0, c1, c2);
+      if (gl == 0) {
+        out[k].c0 = c0;
+        out[k].c1 = c1;
+        c2out[k] = c2;
+      }
+      k++;
+    }
+  }
+}
+
+// LINE_K lanes per G2 point: the 68 raw lines (c2 into `scratch`, count x 68 Fq2), normalised by
+// k_normalise_lines.  With `dec_st` (ciphertext points), the group of point 2j also
 // settles ct_ok[j]: U_j and W_j must decode (threshold_crypto deserialisation); otherwise H_j is
 // replaced by the identity and the proposer's checks are gated off.
 __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
                                                       line_pre* __restrict__ lines, fq2* __restrict__ scratch,
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
                                                       uint8_t* __restrict__ ct_ok) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= count) return;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = gid / LINE_K;
+  const int gl = (int)(gid % LINE_K);
+  const int gbase = (int)(threadIdx.x & 63) - gl;
+  if (k >= count) return;  // whole groups (LINE_K | 64)
   g2a q = pts[k];
   if (dec_st) {
     const uint32_t j = k >> 1;
     const int32_t su = dec_st[j], sw = dec_st[p + j];
     const bool ok = (su == HBX_PT_OK || su == HBX_PT_INFINITY) && (sw == HBX_PT_OK || sw == HBX_PT_INFINITY);
     if ((k & 1) == 0) {
-      ct_ok[j] = ok ? 1 : 0;
+      if (gl == 0) ct_ok[j] = ok ? 1 : 0;
       if (!ok) {
         q.x = fq2_zero();
         q.y = fq2_zero();
         q.inf = true;
-        pts[k] = q;
+        if (gl == 0) pts[k] = q;
       }
     }
   }
   if (q.inf) {
-    for (int i = 0; i < MILLER_LINES; i++) {
-      lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
-      lines[(size_t)k * MILLER_LINES + i].c1 = fq2_zero();
-      scratch[(size_t)k * MILLER_LINES + i] = fq2_one();
+    if (gl == 0) {
+      for (int i = 0; i < MILLER_LINES; i++) {
+        lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
+        lines[(size_t)k * MILLER_LINES + i].c1 = fq2_zero();
+        scratch[(size_t)k * MILLER_LINES + i] = fq2_one();
+      }
     }
     return;
   }
-  g2_raw_lines(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES);
+  g2_raw_lines_group(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES, gl, gbase);
 }
 
 // Second half of the line preparation: one lane per raw line, (c0, c1) /= c2.  68 independent
