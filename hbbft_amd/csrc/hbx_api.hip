@@ -58,7 +58,7 @@ struct hbx_ctx {
   // own-share mode (hbx_set_own_share): this node's index and secret share (8 LE limbs), and its
   // own decryption shares of the prepared ciphertexts
   uint32_t own_me = UINT32_MAX;
-  dbuf own_sk, own_S;
+  dbuf own_sk, own_S, own_part;
   bool own_ready = false;  // own_S computed by the last prepare
   bool ct_known = false;  // ct_valid computed (else deferred into the next share verification)
   const uint8_t* d_v_blob = nullptr;  // device V blob used by the combine (caller-owned for _d)
@@ -349,7 +349,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S};
+                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -420,21 +420,24 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   {
     timed t_(c, HBX_K_PREPARE_CT, s);
     const uint32_t hash_blocks = (uint32_t)(((size_t)p * HASH_K + 63) / 64);
-    const uint32_t dec_blocks = (2 * p + 63) / 64;
     const bool own = c->own_me != UINT32_MAX;
-    if (own && !c->own_S.ensure((size_t)p * sizeof(g1a)))
+    const uint32_t dec_blocks = ((own ? 4 : 2) * p + 63) / 64;
+    if (own && (!c->own_S.ensure((size_t)p * sizeof(g1a)) || !c->own_part.ensure((size_t)2 * p * sizeof(g1j))))
       return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
     hipLaunchKernelGGL(k_prepare_ct, dim3(hash_blocks + dec_blocks), b64, 0, s, d_u_comp, d_v_blob, d_v_off,
                        d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
-                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_S.as<g1a>() : nullptr);
+                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr);
     c->own_ready = own;
   }
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((2 * p * LINE_K + 63) / 64), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
+    const bool own = c->own_ready;
+    const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
+    hipLaunchKernelGGL(k_prepare_lines, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
-                       c->ct_ok.as<uint8_t>());
+                       c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
+                       own ? c->own_S.as<g1a>() : nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = 2 * p * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), b64, 0, s, c->lines.as<line_pre>(),
@@ -652,7 +655,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
-                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr);
+                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),

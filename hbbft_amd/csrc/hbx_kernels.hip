@@ -59,7 +59,8 @@ constexpr int HASH_K = 16;
 //  * blocks [0, hash_blocks): HASH_K-lane groups, one per proposer (hash_g2_group); the hash reads
 //    only the compressed bytes of U_j, so it does not wait for the decode;
 //  * blocks [hash_blocks, ...): one lane per point decodes U_j (j < p) or W_j (p <= j < 2p), in
-//    waves of their own, concurrently with the hash waves.
+//    waves of their own, concurrently with the hash waves; in own-share mode lanes [2p, 4p)
+//    compute the two GLV halves of sk_me U_j (summed by k_prepare_lines).
 // ct_ok and the identity substitution for undecodable ciphertexts (H_j = O) are applied by
 // k_prepare_lines, which runs after both.
 __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u_comp,
@@ -68,7 +69,7 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    const uint8_t* __restrict__ w_comp, uint32_t p,
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
                                                    g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
-                                                   const uint32_t* __restrict__ own_sk, g1a* __restrict__ own_S) {
+                                                   const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part) {
   if (blockIdx.x >= hash_blocks) {
     // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2)
     const uint32_t k = (blockIdx.x - hash_blocks) * blockDim.x + threadIdx.x;
@@ -78,22 +79,21 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
       if (st == HBX_PT_OK && !g1_is_torsion_free(u)) st = HBX_PT_NOT_IN_SUBGROUP;
       dec_st[k] = st;
       U[k] = u;
-      if (own_sk) {
-        // this node's own decryption share sk_me * U_j (decrypt_share_no_verify,
-        // honey_badger.rs:403), GLV: k = k1 + k2 lambda, phi(x, y) = (beta x, y)
-        g1a sh;
-        sh.x = fq_zero();
-        sh.y = fq_zero();
-        sh.inf = true;
-        if (st == HBX_PT_OK) {
-          uint32_t k1[4], k2[4];
-          g1_glv_split(own_sk, k1, k2);
-          g1a up = u;
-          up.x = fq_mul(up.x, fq_from_const(G1_BETA));
-          sh = g1_to_affine(g1_add(g1_mul_u128(u, k1), g1_mul_u128(up, k2)));
-        }
-        own_S[k] = sh;
+    } else if (own_sk && k >= 2 * p && k < 4 * p) {
+      // this node's own decryption share sk_me * U_j (decrypt_share_no_verify,
+      // honey_badger.rs:403), GLV k = k1 + k2 lambda, phi(x, y) = (beta x, y), one half per lane:
+      // lane 2j computes k1 U_j, lane 2j + 1 computes k2 phi(U_j), each decoding U_j itself so
+      // neither waits for the subgroup check (k_prepare_lines adds the halves where U_j is valid)
+      const uint32_t h = k - 2 * p, j = h >> 1;
+      g1a u;
+      g1j part = g1_identity();
+      if (g1_decompress(u_comp + (size_t)j * 48, u) == HBX_PT_OK) {
+        uint32_t k1[4], k2[4];
+        g1_glv_split(own_sk, k1, k2);
+        if (h & 1) u.x = fq_mul(u.x, fq_from_const(G1_BETA));
+        part = g1_mul_u128(u, (h & 1) ? k2 : k1);
       }
+      own_part[h] = part;
     } else if (k < 2 * p) {
       const uint32_t j = k - p;
       g2a w;
@@ -220,7 +220,21 @@ __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int 
 __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
                                                       line_pre* __restrict__ lines, fq2* __restrict__ scratch,
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
-                                                      uint8_t* __restrict__ ct_ok) {
+                                                      uint8_t* __restrict__ ct_ok, const g1j* __restrict__ own_part,
+                                                      g1a* __restrict__ own_S) {
+  const uint32_t line_blocks = (count * LINE_K + 63) / 64;
+  if (blockIdx.x >= line_blocks) {
+    // own share S_j,me = k1 U_j + k2 phi(U_j) (k_prepare_ct's two halves) where U_j decoded
+    const uint32_t j = (blockIdx.x - line_blocks) * blockDim.x + threadIdx.x;
+    if (j >= p) return;
+    g1a sh;
+    sh.x = fq_zero();
+    sh.y = fq_zero();
+    sh.inf = true;
+    if (dec_st[j] == HBX_PT_OK) sh = g1_to_affine(g1_add(own_part[2 * j], own_part[2 * j + 1]));
+    own_S[j] = sh;
+    return;
+  }
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t k = gid / LINE_K;
   const int gl = (int)(gid % LINE_K);
