@@ -233,6 +233,18 @@ __device__ __forceinline__ fq fq_sel8(int s, const fq& v0, const fq& v1, const f
   }
   return r;
 }
+__device__ __forceinline__ fq fq_sel16(int s, const fq (&v)[16]) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint32_t t = v[0].l[i];
+#pragma unroll
+    for (int k = 1; k < 16; k++) t = (s == k) ? v[k].l[i] : t;
+    r.l[i] = t;
+  }
+  return r;
+}
+
 __device__ __noinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
   const int s = gl & 7;
   const fq x0 = p.x.c0, x1 = p.x.c1, y0 = p.y.c0, y1 = p.y.c1, z0 = p.z.c0, z1 = p.z.c1;
@@ -266,46 +278,133 @@ __device__ __forceinline__ g2j g2_dbl_n_group(g2j p, int n, int gl, int gbase) {
   for (int i = 0; i < n; i++) p = g2_dbl_group(p, gl, gbase);
   return p;
 }
-// g2_mul_u64 / g2_mul_gls_d / g2_clear_cofactor (curve.hpp) with the group doubling
+// g2_add (add-2007-bl) on 16 lanes of a group holding the same p and q: its 16 Fq2 products
+// (43 Fq products) as five rounds of independent Fq products, one per lane.  Same special cases
+// as g2_add (identities, P = Q, P = -Q), decided group-uniformly.
+struct round16 {
+  fq a[16], b[16];
+};
+__device__ __forceinline__ void r16_mul(round16& R, int k, const fq2& x, const fq2& y) {
+  R.a[k] = x.c0; R.b[k] = y.c0;
+  R.a[k + 1] = x.c1; R.b[k + 1] = y.c1;
+  R.a[k + 2] = x.c0; R.b[k + 2] = y.c1;
+  R.a[k + 3] = x.c1; R.b[k + 3] = y.c0;
+}
+__device__ __forceinline__ void r16_sqr(round16& R, int k, const fq2& x) {
+  R.a[k] = fq_add(x.c0, x.c1); R.b[k] = fq_sub(x.c0, x.c1);
+  R.a[k + 1] = x.c0; R.b[k + 1] = x.c1;
+}
+__device__ __forceinline__ fq r16_run(const round16& R, int gl) { return fq_mul(fq_sel16(gl, R.a), fq_sel16(gl, R.b)); }
+__device__ __forceinline__ fq2 r16_get_mul(const fq& r, int k, int gbase) {
+  return fq2{fq_sub(fq_from_lane(r, gbase + k), fq_from_lane(r, gbase + k + 1)),
+             fq_add(fq_from_lane(r, gbase + k + 2), fq_from_lane(r, gbase + k + 3))};
+}
+__device__ __forceinline__ fq2 r16_get_sqr(const fq& r, int k, int gbase) {
+  return fq2{fq_from_lane(r, gbase + k), fq_dbl(fq_from_lane(r, gbase + k + 1))};
+}
+__device__ __forceinline__ void r16_clear(round16& R) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    R.a[i] = fq_zero();
+    R.b[i] = fq_zero();
+  }
+}
+__device__ __noinline__ g2j g2_add_group(const g2j& p, const g2j& q, int gl, int gbase) {
+  if (g2j_is_identity(p)) return q;
+  if (g2j_is_identity(q)) return p;
+  round16 R;
+  r16_clear(R);
+  // round 1: Z1^2, Z2^2, Y1 Z2, Y2 Z1, (Z1 + Z2)^2
+  r16_sqr(R, 0, p.z);
+  r16_sqr(R, 2, q.z);
+  r16_mul(R, 4, p.y, q.z);
+  r16_mul(R, 8, q.y, p.z);
+  r16_sqr(R, 12, fq2_add(p.z, q.z));
+  fq r = r16_run(R, gl);
+  const fq2 Z1Z1 = r16_get_sqr(r, 0, gbase), Z2Z2 = r16_get_sqr(r, 2, gbase);
+  const fq2 Y1Z2 = r16_get_mul(r, 4, gbase), Y2Z1 = r16_get_mul(r, 8, gbase);
+  const fq2 ZS = r16_get_sqr(r, 12, gbase);
+  // round 2: U1, U2, S1, S2
+  r16_mul(R, 0, p.x, Z2Z2);
+  r16_mul(R, 4, q.x, Z1Z1);
+  r16_mul(R, 8, Y1Z2, Z2Z2);
+  r16_mul(R, 12, Y2Z1, Z1Z1);
+  r = r16_run(R, gl);
+  const fq2 U1 = r16_get_mul(r, 0, gbase), U2 = r16_get_mul(r, 4, gbase);
+  const fq2 S1 = r16_get_mul(r, 8, gbase), S2 = r16_get_mul(r, 12, gbase);
+  if (fq2_eq(U1, U2)) {
+    if (fq2_eq(S1, S2)) return g2_dbl_group(p, gl, gbase);
+    return g2_identity();
+  }
+  const fq2 H = fq2_sub(U2, U1);
+  const fq2 rr = fq2_dbl(fq2_sub(S2, S1));
+  // round 3: I = (2H)^2, r^2, Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
+  r16_sqr(R, 0, fq2_dbl(H));
+  r16_sqr(R, 2, rr);
+  r16_mul(R, 4, fq2_sub(fq2_sub(ZS, Z1Z1), Z2Z2), H);
+  r = r16_run(R, gl);
+  const fq2 I = r16_get_sqr(r, 0, gbase), RR = r16_get_sqr(r, 2, gbase), Z3 = r16_get_mul(r, 4, gbase);
+  // round 4: J = H I, V = U1 I
+  r16_mul(R, 0, H, I);
+  r16_mul(R, 4, U1, I);
+  r = r16_run(R, gl);
+  const fq2 J = r16_get_mul(r, 0, gbase), V = r16_get_mul(r, 4, gbase);
+  const fq2 X3 = fq2_sub(fq2_sub(RR, J), fq2_dbl(V));
+  // round 5: r (V - X3), S1 J
+  r16_mul(R, 0, rr, fq2_sub(V, X3));
+  r16_mul(R, 4, S1, J);
+  r = r16_run(R, gl);
+  const fq2 Y3 = fq2_sub(r16_get_mul(r, 0, gbase), fq2_dbl(r16_get_mul(r, 4, gbase)));
+  return g2j{X3, Y3, Z3};
+}
+__device__ __forceinline__ g2j g2_sub_group(const g2j& p, const g2j& q, int gl, int gbase) {
+  return g2_add_group(p, g2_neg(q), gl, gbase);
+}
+
+// g2_mul_u64 / g2_mul_gls_d / g2_clear_cofactor (curve.hpp) with the group doubling and addition
+#define GADD(a, b) g2_add_group(a, b, gl, gbase)
+#define GSUB(a, b) g2_sub_group(a, b, gl, gbase)
 __device__ g2j g2_mul_u64_group(const g2j& p, uint64_t k, int gl, int gbase) {
   g2j acc = p;
   const int top = 63 - __builtin_clzll(k);
   for (int i = top - 1; i >= 0; i--) {
     acc = g2_dbl_group(acc, gl, gbase);
-    if ((k >> i) & 1) acc = g2_add(acc, p);
+    if ((k >> i) & 1) acc = GADD(acc, p);
   }
   return acc;
 }
 __device__ g2j g2_mul_gls_d_group(const g2j& P, int gl, int gbase) {
   const g2j P2 = g2_dbl_group(P, gl, gbase);
   const g2j P4 = g2_dbl_group(P2, gl, gbase);
-  g2j Z = g2_add(P4, P);
-  Z = g2_add(g2_dbl_n_group(Z, 4, gl, gbase), Z);
-  Z = g2_add(g2_dbl_n_group(Z, 8, gl, gbase), Z);
-  const g2j W = g2_add(g2_dbl_group(Z, gl, gbase), P);
-  g2j acc = g2_add(g2_dbl_n_group(P2, 3, gl, gbase), P);
-  acc = g2_add(g2_dbl_group(acc, gl, gbase), P);
+  g2j Z = GADD(P4, P);
+  Z = GADD(g2_dbl_n_group(Z, 4, gl, gbase), Z);
+  Z = GADD(g2_dbl_n_group(Z, 8, gl, gbase), Z);
+  const g2j W = GADD(g2_dbl_group(Z, gl, gbase), P);
+  g2j acc = GADD(g2_dbl_n_group(P2, 3, gl, gbase), P);
+  acc = GADD(g2_dbl_group(acc, gl, gbase), P);
   acc = g2_dbl_n_group(acc, 1 + 8 + 16, gl, gbase);
-  acc = g2_add(acc, Z);
-  acc = g2_add(g2_dbl_n_group(acc, 16, gl, gbase), Z);
-  return g2_add(g2_dbl_n_group(acc, 16, gl, gbase), W);
+  acc = GADD(acc, Z);
+  acc = GADD(g2_dbl_n_group(acc, 16, gl, gbase), Z);
+  return GADD(g2_dbl_n_group(acc, 16, gl, gbase), W);
 }
 __device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
   const g2j t1 = g2_neg(g2_mul_u64_group(P, BLS_X, gl, gbase));
   g2j t2 = g2_psi(P);
   g2j t3 = g2_psi(g2_psi(g2_dbl_group(P, gl, gbase)));
-  t3 = g2_sub(t3, t2);
-  t2 = g2_add(t1, t2);
+  t3 = GSUB(t3, t2);
+  t2 = GADD(t1, t2);
   t2 = g2_neg(g2_mul_u64_group(t2, BLS_X, gl, gbase));
-  t3 = g2_add(t3, t2);
-  t3 = g2_sub(t3, t1);
-  const g2j Q = g2_sub(t3, P);
+  t3 = GADD(t3, t2);
+  t3 = GSUB(t3, t1);
+  const g2j Q = GSUB(t3, P);
   const g2j q1 = g2_psi(Q);
   const g2j q2 = g2_psi(q1);
   const g2j q3 = g2_psi(q2);
-  const g2j Rp = g2_sub(g2_sub(g2_add(Q, q1), q2), q3);
+  const g2j Rp = GSUB(GSUB(GADD(Q, q1), q2), q3);
   return g2_mul_gls_d_group(Rp, gl, gbase);
 }
+#undef GADD
+#undef GSUB
 
 // hash_g2 by a GROUP of K aligned lanes of one wave (K | 64), same point as g2_rand_from_rng.
 //

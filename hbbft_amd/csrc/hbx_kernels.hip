@@ -118,18 +118,6 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
 // Lanes per G2 point in k_prepare_lines.
 constexpr int LINE_K = 16;
 
-__device__ __forceinline__ fq fq_sel16(int s, const fq (&v)[16]) {
-  fq r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint32_t t = v[0].l[i];
-#pragma unroll
-    for (int k = 1; k < 16; k++) t = (s == k) ? v[k].l[i] : t;
-    r.l[i] = t;
-  }
-  return r;
-}
-
 // line_dbl_step (pairing.hpp) on the LINE_K lanes of a group that all hold T: its 26 Fq
 // products as three rounds of independent products, one per lane (10, 14 and 8 lanes busy),
 // exchanged by ds_bpermute; Fq2 products by schoolbook.  Same values mod p as line_dbl_step.
