@@ -44,3 +44,22 @@ def test_sign_matches_honest_shares(hbx_ctx):
     sigs = hbx_ctx.sign(d["sk"])
     honest = d["expect_valid"]
     np.testing.assert_array_equal(sigs[honest], d["sigs"][honest])
+
+
+@pytest.mark.gpu
+def test_hash_g2_many_nonces_vs_oracle(hbx_ctx):
+    """hash_g2 (threshold_crypto G2::rand from a SHA-256-seeded ChaChaRng, full cofactor) for 256
+    random messages of 0..1100 bytes, through the group kernel (16-candidate residuosity test,
+    cofactor clearing on 8-16 cooperating lanes), against the oracle's sequential hash_g2: the
+    compressed points must be identical."""
+    import random
+
+    from oracle import bls12_381 as bls
+    from oracle import threshold as tc
+
+    rnd = random.Random(2024)
+    lens = [0, 1, 32, 63, 64, 65, 128, 1100] + [rnd.randrange(0, 1100) for _ in range(248)]
+    msgs = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
+    h = hbx_ctx.prepare_nonces(msgs)
+    for j, m in enumerate(msgs):
+        assert bytes(h[j]) == bls.g2_compress(tc.hash_g2(m)), f"message {j} (len {len(m)})"
