@@ -191,8 +191,8 @@ def main():
     if not args.no_own_share:
         ctx.set_own_share(OWN_INDEX, ep["own_sk"])
 
-    # a dedicated stream: torch's default stream is the NULL handle, which the C ABI maps to the
-    # context's own stream -- HIP events must be recorded on the stream the kernels run on
+    # a dedicated stream for the epoch calls; the HIP events that time the epoch and the kernels are
+    # recorded on the stream the kernels run on
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
@@ -221,8 +221,8 @@ def main():
     def step(events=None):
         if events:
             events[0].record(stream)
-        # one call per node-epoch (hbx_decrypt_epoch_d): hash_g1_g2 + lines, share checks, then
-        # Ciphertext::verify on the context's second stream beside the speculative combine, decrypt
+        # one call per node-epoch (hbx_decrypt_epoch_d): hash_g1_g2 + lines, share checks (the
+        # node's own share check is Ciphertext::verify), combine + decrypt
         ctx.decrypt_epoch_d(d_u, d_v, d_off, d_w, pj, maxv, d_shares, n, t, d_out, d_valid=d_valid,
                             d_ct_valid=d_ct_valid, d_status=d_status, stream=sh)
         if events:

@@ -1,6 +1,7 @@
 // Broadcast byte path on gfx950: Reed-Solomon
 // GF(2^8) coding as reed-solomon-erasure 3.1.0 defines it and the SHA-256 Merkle tree of the
-// afck/merkle.rs fork, for whole batches of broadcast instances (reference src/broadcast.rs).
+// afck/merkle.rs fork (or the opt-in SHA3-256 tree of later hbbft), for whole batches of
+// broadcast instances (reference src/broadcast.rs).
 //
 // HBM layout: one instance = n shards of L bytes, contiguous ([inst][n][L]); leaf i of an
 // instance is the index byte i followed by shard i (broadcast.rs:373-377), never materialised.
@@ -267,6 +268,53 @@ __device__ void sha256_prefixed(uint32_t prefix, int plen, const uint8_t* data, 
   for (int i = 0; i < 8; i++) h8[i] = s.h[i];
 }
 
+// SHA3-256 of (prefix bytes) || data[len] (the SHA3 Merkle variant's leaf: SHA3(index byte ||
+// shard)), one lane; full 136-byte blocks of data are read as aligned dwords realigned with
+// v_alignbyte (little-endian lanes, no byte swap).  Digest as 8 big-endian words like
+// sha256_prefixed, so both variants share the tree and output code.
+__device__ void sha3_prefixed(uint32_t prefix, int plen, const uint8_t* data, uint64_t len, uint32_t* h8) {
+  uint64_t st[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) st[i] = 0;
+  const uint64_t total = (uint64_t)plen + len;
+  const uint64_t nblocks = total / 136 + 1;
+  for (uint64_t blk = 0; blk < nblocks; blk++) {
+    const uint64_t b0 = blk * 136;
+    if (b0 >= (uint64_t)plen && b0 + 136 <= total) {
+      const uint8_t* q = data + (b0 - plen);
+      const uintptr_t a = (uintptr_t)q;
+      const uint32_t* pa = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3);
+      uint32_t d[35];
+      const int nd = sh ? 35 : 34;
+#pragma unroll
+      for (int i = 0; i < 35; i++) d[i] = i < nd ? pa[i] : 0;
+#pragma unroll
+      for (int i = 0; i < 17; i++) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * i + 1], d[2 * i], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * i + 2], d[2 * i + 1], sh);
+        st[i] ^= (uint64_t)lo | ((uint64_t)hi << 32);
+      }
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < 17; i++) {
+        uint64_t lane = 0;
+        for (int k = 0; k < 8; k++) {
+          const uint64_t pos = b0 + 8 * i + k;
+          uint8_t byte = pos < total ? msg_byte(prefix, plen, data, len, pos) : 0;
+          if (pos == total) byte ^= 0x06;
+          if (blk == nblocks - 1 && 8 * i + k == 135) byte ^= 0x80;
+          lane |= (uint64_t)byte << (8 * k);
+        }
+        st[i] ^= lane;
+      }
+    }
+    keccak_f1600(st);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) h8[i] = bswap32((uint32_t)(st[i >> 1] >> (32 * (i & 1))));
+}
+
 // node = SHA-256(0x01 || left || right) on big-endian word digests (2 blocks)
 __device__ void sha256_node(const uint32_t* l8, const uint32_t* r8, uint32_t* out8) {
   sha256_state s;
@@ -289,48 +337,171 @@ __device__ void sha256_node(const uint32_t* l8, const uint32_t* r8, uint32_t* ou
   for (int i = 0; i < 8; i++) out8[i] = s.h[i];
 }
 
-// Leaf hashes of the index-prefixed shards: leaf(i) = SHA-256(0x00 || i || shard_i).
+// node = SHA3-256(left || right) (the SHA3 Merkle variant: no domain prefixes)
+__device__ void sha3_node(const uint32_t* l8, const uint32_t* r8, uint32_t* out8) {
+  uint64_t st[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) st[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    st[i] = (uint64_t)bswap32(l8[2 * i]) | ((uint64_t)bswap32(l8[2 * i + 1]) << 32);
+    st[4 + i] = (uint64_t)bswap32(r8[2 * i]) | ((uint64_t)bswap32(r8[2 * i + 1]) << 32);
+  }
+  st[8] = 0x06;                      // padding right after the 64 message bytes
+  st[16] = 0x8000000000000000ull;    // last byte of the 136-byte block
+  keccak_f1600(st);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out8[i] = bswap32((uint32_t)(st[i >> 1] >> (32 * (i & 1))));
+}
+
+// Merkle digests by variant (include/hbx.h HBX_MERKLE_*):
+//   HBX_MERKLE_SHA256  merkle (afck fork) + ring: leaf SHA-256(0x00 || v), node SHA-256(0x01 || l || r)
+//   HBX_MERKLE_SHA3    later hbbft's merkle.rs:  leaf SHA3-256(v),         node SHA3-256(l || r)
+// Leaves of the broadcast are index-prefixed shards: v = [i as u8] || shard_i (broadcast.rs:373-377).
+constexpr int MERKLE_SHA256 = 0;
+constexpr int MERKLE_SHA3 = 1;
+__device__ __forceinline__ void merkle_leaf_shard(int variant, uint32_t i, const uint8_t* shard, uint64_t L, uint32_t* h) {
+  if (variant == MERKLE_SHA3) sha3_prefixed(i & 0xFF, 1, shard, L, h);
+  else sha256_prefixed((i & 0xFF) << 8, 2, shard, L, h);
+}
+__device__ __forceinline__ void merkle_leaf_value(int variant, const uint8_t* v, uint64_t len, uint32_t* h) {
+  if (variant == MERKLE_SHA3) sha3_prefixed(0, 0, v, len, h);
+  else sha256_prefixed(0, 1, v, len, h);
+}
+__device__ __forceinline__ void merkle_node(int variant, const uint32_t* l8, const uint32_t* r8, uint32_t* out8) {
+  if (variant == MERKLE_SHA3) sha3_node(l8, r8, out8);
+  else sha256_node(l8, r8, out8);
+}
+
+// Leaf hashes of the index-prefixed shards: leaf(i) = H_leaf([i] || shard_i).
 // grid (ceil(n/64), inst); out: u32[inst][n][8] (digest words, big-endian order).
 __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict__ shards, size_t inst_stride,
-                                                      uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash) {
+                                                      uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
+                                                      int variant) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t inst = blockIdx.y;
   if (i >= n) return;
   uint32_t h[8];
-  sha256_prefixed((i & 0xFF) << 8, 2, shards + (size_t)inst * inst_stride + (size_t)i * L, L, h);
+  merkle_leaf_shard(variant, i, shards + (size_t)inst * inst_stride + (size_t)i * L, L, h);
   uint32_t* o = leaf_hash + ((size_t)inst * n + i) * 8;
 #pragma unroll
   for (int q = 0; q < 8; q++) o[q] = h[q];
 }
 
+// Number of stored tree nodes for n leaves: every level from the leaves (n) to the root (1),
+// with a promoted odd node stored again on the level it moves to.
+__host__ __device__ inline uint32_t merkle_node_count(uint32_t n) {
+  uint32_t total = 0, c = n;
+  while (true) {
+    total += c;
+    if (c <= 1) break;
+    c = (c + 1) / 2;
+  }
+  return total;
+}
+
 // MerkleTree::from_vec levels (pairs left to right, odd trailing node promoted): one block per
-// instance, the level in LDS.  roots: u8[inst][32].
+// instance, the level in LDS.  roots: u8[inst][32]; nodes (optional): u8[inst][node_count][32],
+// level-major from the leaf level up, the root last (the `(2n - 1) x 32` tree of SURVEY.md
+// §8(b) hbx_merkle_build, plus the promoted copies).
 __global__ void __launch_bounds__(128) k_merkle_tree(const uint32_t* __restrict__ leaf_hash, uint32_t n,
-                                                     uint8_t* __restrict__ roots) {
+                                                     uint8_t* __restrict__ roots, uint8_t* __restrict__ nodes,
+                                                     int variant) {
   __shared__ uint32_t lvl[2][RS_MAX_N][8];
   const uint32_t inst = blockIdx.x;
   for (uint32_t e = threadIdx.x; e < n * 8; e += blockDim.x) lvl[0][e / 8][e % 8] = leaf_hash[(size_t)inst * n * 8 + e];
   __syncthreads();
-  uint32_t cnt = n;
+  uint8_t* out = nodes ? nodes + (size_t)inst * merkle_node_count(n) * 32 : nullptr;
+  auto store = [&](int cur, uint32_t cnt, uint32_t base) {
+    if (!out) return;
+    for (uint32_t e = threadIdx.x; e < cnt * 32; e += blockDim.x) {
+      const uint32_t wv = lvl[cur][e / 32][(e % 32) / 4];
+      out[(size_t)(base + e / 32) * 32 + e % 32] = (uint8_t)(wv >> (8 * (3 - e % 4)));
+    }
+  };
+  uint32_t cnt = n, base = 0;
   int cur = 0;
+  store(cur, cnt, base);
   while (cnt > 1) {
     const uint32_t nxt = (cnt + 1) / 2;
     for (uint32_t j = threadIdx.x; j < nxt; j += blockDim.x) {
       if (2 * j + 1 < cnt) {
-        sha256_node(lvl[cur][2 * j], lvl[cur][2 * j + 1], lvl[cur ^ 1][j]);
+        merkle_node(variant, lvl[cur][2 * j], lvl[cur][2 * j + 1], lvl[cur ^ 1][j]);
       } else {
 #pragma unroll
         for (int q = 0; q < 8; q++) lvl[cur ^ 1][j][q] = lvl[cur][2 * j][q];
       }
     }
     __syncthreads();
+    base += cnt;
     cur ^= 1;
     cnt = nxt;
+    store(cur, cnt, base);
   }
   if (threadIdx.x < 32) {
     const uint32_t wv = lvl[cur][0][threadIdx.x / 4];
     roots[(size_t)inst * 32 + threadIdx.x] = (uint8_t)(wv >> (8 * (3 - threadIdx.x % 4)));
   }
+}
+
+// MerkleTree::gen_proof (broadcast.rs:389-401 asks one per node) from the stored tree: proof q
+// is for leaf req[2q + 1] of instance req[2q]; like merkle.rs it is the proof of the FIRST leaf
+// whose digest equals that leaf's (equal leaves cannot occur for index-prefixed shards of N <= 256,
+// broadcast.rs:371-372, but the semantics are kept).  Output in the layout k_merkle_validate
+// reads: node path root first ... leaf digest (depth + 1 entries of 32 B), the sibling of each
+// lemma level, `sides` bit l = the level-l sibling is Positioned::Left, depth, root.
+__global__ void __launch_bounds__(64) k_merkle_proofs(const uint8_t* __restrict__ nodes, uint32_t n,
+                                                      const uint32_t* __restrict__ req, uint32_t count,
+                                                      uint8_t* __restrict__ node_hash, uint8_t* __restrict__ sib_hash,
+                                                      uint32_t* __restrict__ sides, uint32_t* __restrict__ depth,
+                                                      uint8_t* __restrict__ root) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= count) return;
+  const uint32_t inst = req[2 * q];
+  uint32_t pos = req[2 * q + 1];
+  const uint32_t total = merkle_node_count(n);
+  const uint8_t* T = nodes + (size_t)inst * total * 32;
+  auto eq32 = [](const uint8_t* a, const uint8_t* b) {
+    bool e = true;
+    for (int k = 0; k < 32; k++) e = e && a[k] == b[k];
+    return e;
+  };
+  for (uint32_t j = 0; j < pos; j++)
+    if (eq32(T + (size_t)j * 32, T + (size_t)pos * 32)) {
+      pos = j;
+      break;
+    }
+  // walk up: (node on the path, sibling, side) for every level where the node has a sibling
+  uint32_t path[16], sib[16], left_bits = 0, d = 0;
+  uint32_t cnt = n, base = 0;
+  while (cnt > 1) {
+    const bool promoted = (pos % 2 == 0) && pos == cnt - 1;
+    if (!promoted) {
+      path[d] = base + pos;
+      sib[d] = base + (pos ^ 1u);
+      if (pos & 1u) left_bits |= 1u << d;  // sibling on the left
+      d++;
+    }
+    base += cnt;
+    pos /= 2;
+    cnt = (cnt + 1) / 2;
+  }
+  const uint32_t root_idx = total - 1;
+  uint8_t* nh = node_hash + (size_t)q * 17 * 32;
+  uint8_t* sh = sib_hash + (size_t)q * 16 * 32;
+  uint32_t side_out = 0;
+  for (int k = 0; k < 32; k++) nh[k] = T[(size_t)root_idx * 32 + k];
+  for (uint32_t lv = 0; lv < d; lv++) {
+    const uint32_t up = d - 1 - lv;  // lemma level lv (root first) = walk step d - 1 - lv
+    for (int k = 0; k < 32; k++) {
+      sh[(size_t)lv * 32 + k] = T[(size_t)sib[up] * 32 + k];
+      nh[(size_t)(lv + 1) * 32 + k] = T[(size_t)path[up] * 32 + k];
+    }
+    if ((left_bits >> up) & 1u) side_out |= 1u << lv;
+  }
+  for (int k = 0; k < 32; k++) root[(size_t)q * 32 + k] = T[(size_t)root_idx * 32 + k];
+  sides[q] = side_out;
+  depth[q] = d;
 }
 
 // Broadcast::validate_proof (broadcast.rs:555-575) over a batch of proofs:
@@ -347,7 +518,7 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
                                                         const uint32_t* __restrict__ depth,
                                                         const uint8_t* __restrict__ root_hash,
                                                         const uint32_t* __restrict__ sender, uint32_t count,
-                                                        uint32_t nproofs, uint8_t* __restrict__ valid) {
+                                                        uint32_t nproofs, uint8_t* __restrict__ valid, int variant) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nproofs) return;
   const uint32_t d = depth[j];
@@ -362,15 +533,15 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
   };
   uint32_t h[8], want[8], a[8], b[8];
   if (ok) {
-    sha256_prefixed(0, 1, val, vlen, h);
+    merkle_leaf_value(variant, val, vlen, h);
     be8(nodes + (size_t)d * 32, want);
     for (int q = 0; q < 8; q++) ok = ok && h[q] == want[q];
   }
   for (uint32_t lv = 0; lv < d && ok; lv++) {
     be8(sibs + (size_t)lv * 32, a);
     be8(nodes + (size_t)(lv + 1) * 32, b);
-    if ((sides[j] >> lv) & 1) sha256_node(a, b, h);
-    else sha256_node(b, a, h);
+    if ((sides[j] >> lv) & 1) merkle_node(variant, a, b, h);
+    else merkle_node(variant, b, a, h);
     be8(nodes + (size_t)lv * 32, want);
     for (int q = 0; q < 8; q++) ok = ok && h[q] == want[q];
   }

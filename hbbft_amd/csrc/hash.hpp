@@ -2,6 +2,7 @@
 //  * SHA-256 (FIPS 180-4) -- the digest threshold_crypto applies inside hash_g2 / hash_g1_g2 /
 //    hash_bytes (DIGEST default = SHA-256, the reference's own `ring`
 //    dependency, Cargo.toml:32) and the Merkle hash of broadcast.rs:381/:683;
+//  * SHA3-256 (FIPS 202) -- the opt-in DIGEST variant (tiny-keccak) and the SHA3 Merkle variant;
 //  * ChaCha20 as `rand 0.4` ChaChaRng emits it (Cargo.toml:29): key = 8 seed words, 128-bit
 //    block counter in words 12..15, words returned in block order, next_u64 = hi<<32 | lo;
 //  * hash_g2 / hash_g1_g2 (threshold_crypto): digest -> 8 big-endian seed words -> ChaChaRng ->
@@ -98,6 +99,95 @@ HBX_HD void sha256_2(const uint8_t* m0, uint64_t n0, const uint8_t* m1, uint64_t
     out32[4 * i + 2] = (uint8_t)(s.h[i] >> 8);
     out32[4 * i + 3] = (uint8_t)s.h[i];
   }
+}
+
+// ----------------------------------------------------------------------------------------------
+// SHA3-256 (FIPS 202): Keccak-f[1600], rate 136 bytes, domain padding 0x06 .. 0x80.
+// The opt-in DIGEST of SURVEY.md App. A.3: threshold_crypto revisions that hash with tiny-keccak's
+// sha3_256 instead of SHA-256 (reference Cargo.toml:35 pins no revision), and the digest of the
+// SHA3 Merkle variant (later hbbft's src/broadcast/merkle.rs).  State: 25 x u64 lanes in
+// registers; every 64-bit rotate is two v_alignbit_b32.
+// ----------------------------------------------------------------------------------------------
+HBX_CONST uint64_t KECCAK_RC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+
+HBX_HD uint64_t rotl64(uint64_t x, int n) { return n == 0 ? x : (x << n) | (x >> (64 - n)); }
+
+// Keccak-f[1600] on a[5 * y + x].
+HBX_HDNI void keccak_f1600(uint64_t* st) {
+  uint64_t a[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) a[i] = st[i];
+  // rho offsets and the pi permutation as one table: b[pi(i)] = rotl(a[i], rho(i))
+  constexpr int RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+#pragma unroll 1
+  for (int r = 0; r < 24; r++) {
+    uint64_t c[5], b[25];
+#pragma unroll
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const uint64_t d = c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+#pragma unroll
+      for (int y = 0; y < 5; y++) a[5 * y + x] ^= d;
+    }
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+      for (int y = 0; y < 5; y++) {
+        // (x, y) -> (y, 2x + 3y)
+        const int X = y, Y = (2 * x + 3 * y) % 5;
+        b[5 * Y + X] = rotl64(a[5 * y + x], RHO[5 * y + x]);
+      }
+#pragma unroll
+    for (int y = 0; y < 5; y++)
+#pragma unroll
+      for (int x = 0; x < 5; x++) a[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
+    a[0] ^= KECCAK_RC[r];
+  }
+#pragma unroll
+  for (int i = 0; i < 25; i++) st[i] = a[i];
+}
+
+// SHA3-256 over a concatenation of up to two byte ranges (like sha256_2), one lane.
+HBX_HD void sha3_256_2(const uint8_t* m0, uint64_t n0, const uint8_t* m1, uint64_t n1, uint8_t* out32) {
+  uint64_t st[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) st[i] = 0;
+  const uint64_t total = n0 + n1;
+  const uint64_t nblocks = total / 136 + 1;  // the padding always fits the last block (>= 1 byte)
+  for (uint64_t blk = 0; blk < nblocks; blk++) {
+    for (int i = 0; i < 17; i++) {
+      uint64_t lane = 0;
+      for (int k = 0; k < 8; k++) {
+        const uint64_t pos = blk * 136 + (uint64_t)(8 * i + k);
+        uint8_t byte;
+        if (pos < n0) byte = m0[pos];
+        else if (pos < total) byte = m1[pos - n0];
+        else byte = 0;
+        if (pos == total) byte ^= 0x06;
+        if (blk == nblocks - 1 && 8 * i + k == 135) byte ^= 0x80;
+        lane |= (uint64_t)byte << (8 * k);
+      }
+      st[i] ^= lane;
+    }
+    keccak_f1600(st);
+  }
+  for (int i = 0; i < 32; i++) out32[i] = (uint8_t)(st[i >> 3] >> (8 * (i & 7)));
+}
+
+// The DIGEST of threshold_crypto's hash_g2 / hash_g1_g2 / hash_bytes (include/hbx.h
+// HBX_DIGEST_*): a per-context switch, SHA-256 by default.
+constexpr int DIGEST_SHA256 = 0;
+constexpr int DIGEST_SHA3_256 = 1;
+HBX_HD void digest2(int variant, const uint8_t* m0, uint64_t n0, const uint8_t* m1, uint64_t n1, uint8_t* out32) {
+  if (variant == DIGEST_SHA3_256) sha3_256_2(m0, n0, m1, n1, out32);
+  else sha256_2(m0, n0, m1, n1, out32);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -477,19 +567,21 @@ HBX_HD g2j hash_g2_from_digest(const uint8_t* d32) {
   return g2_rand_from_rng(r);
 }
 
-// hash_g1_g2(u, v): m = (|v| > 64 ? SHA256(v) : v) || u_comp48; H = hash_g2(m).
-HBX_HD void hash_g1_g2_digest(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen, uint8_t* d) {
+// hash_g1_g2(u, v): m = (|v| > 64 ? DIGEST(v) : v) || u_comp48; H = hash_g2(m), whose seed is
+// DIGEST(m).
+HBX_HD void hash_g1_g2_digest(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen, uint8_t* d,
+                              int variant = DIGEST_SHA256) {
   if (vlen > 64) {
     uint8_t dv[32];
-    sha256_2(v, vlen, nullptr, 0, dv);
-    sha256_2(dv, 32, u_comp48, 48, d);
+    digest2(variant, v, vlen, nullptr, 0, dv);
+    digest2(variant, dv, 32, u_comp48, 48, d);
   } else {
-    sha256_2(v, vlen, u_comp48, 48, d);
+    digest2(variant, v, vlen, u_comp48, 48, d);
   }
 }
-HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen) {
+HBX_HD g2j hash_g1_g2(const uint8_t* u_comp48, const uint8_t* v, uint64_t vlen, int variant = DIGEST_SHA256) {
   uint8_t d[32];
-  hash_g1_g2_digest(u_comp48, v, vlen, d);
+  hash_g1_g2_digest(u_comp48, v, vlen, d, variant);
   return hash_g2_from_digest(d);
 }
 

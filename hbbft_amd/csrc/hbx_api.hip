@@ -49,6 +49,8 @@ struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err = "ok";
+  int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
+  int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
   // era state
   uint32_t n_keys = 0;
   dbuf pk, pk_status, pk_comp;
@@ -65,8 +67,9 @@ struct hbx_ctx {
   const uint64_t* d_v_off = nullptr;
   uint64_t max_v_len = 0;
   dbuf v_blob_own, v_off_own, u_comp_own, w_comp_own;
-  // verification state
-  uint32_t n_shares = 0;
+  // verification state: n_shares / verified_p of the last verify after the latest prepare
+  // (0 = none: a prepare invalidates S / valid for the combine)
+  uint32_t n_shares = 0, verified_p = 0;
   dbuf S, S_status, fallback, valid, shares_own, present_own;
   // combine state
   dbuf keys, status, out_own;
@@ -137,12 +140,15 @@ static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(ctx, HBX_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
-static hipStream_t pick(hbx_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+// _d API: the caller's stream; NULL is the HIP null stream (a framework's default stream), so the
+// enqueued work is ordered with the caller's own work on it.
+static hipStream_t pick(hbx_ctx*, void* s) { return static_cast<hipStream_t>(s); }
 
+// bit k = (bytes[k] == 1): status bytes (HBX_SHARE_VALID, HBX_CT_VALID) and 0/1 flags alike
 static void pack_bits(const uint8_t* bytes, size_t n, uint8_t* bits) {
   memset(bits, 0, (n + 7) / 8);
   for (size_t k = 0; k < n; k++)
-    if (bytes[k]) bits[k >> 3] |= (uint8_t)(1u << (k & 7));
+    if (bytes[k] == 1) bits[k >> 3] |= (uint8_t)(1u << (k & 7));
 }
 
 static bool scalars_canonical(const uint8_t* s32, size_t count);
@@ -295,16 +301,17 @@ static int rs_reconstruct(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_presen
 }
 
 static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* d_roots,
-                        hipStream_t s) {
+                        hipStream_t s, uint8_t* d_nodes = nullptr) {
   if (n == 0 || n > (uint32_t)RS_MAX_N) return fail(c, HBX_E_INVALID_ARG, "merkle: need 1 <= n <= 256");
   if (!c->leaf_hash.ensure((size_t)inst * n * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: leaf hashes");
   {
     timed t_(c, HBX_K_MERKLE_LEAVES, s);
     hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                       c->leaf_hash.as<uint32_t>());
+                       c->leaf_hash.as<uint32_t>(), c->merkle);
   }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots);
+  hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots, d_nodes,
+                     c->merkle);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -356,9 +363,40 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   return HBX_OK;
 }
 
+int hbx_set_digest(hbx_ctx* c, int variant) {
+  if (!c || (variant != HBX_DIGEST_SHA256 && variant != HBX_DIGEST_SHA3_256))
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_digest: unknown variant %d", variant);
+  c->digest = variant == HBX_DIGEST_SHA3_256 ? DIGEST_SHA3_256 : DIGEST_SHA256;
+  c->p_ct = 0;  // hashes prepared under the other digest are void
+  c->ct_known = false;
+  c->n_shares = 0;
+  c->verified_p = 0;
+  c->coin_I = 0;
+  c->coin_n = 0;
+  return HBX_OK;
+}
+
+int hbx_set_merkle_digest(hbx_ctx* c, int variant) {
+  if (!c || (variant != HBX_MERKLE_SHA256 && variant != HBX_MERKLE_SHA3))
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_merkle_digest: unknown variant %d", variant);
+  c->merkle = variant;
+  return HBX_OK;
+}
+
 int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* status) {
   if (!c || (!pk_comp && n)) return fail(c, HBX_E_INVALID_ARG, "hbx_set_pk_shares: bad args");
   HIPCHK(c, hipSetDevice(c->device));
+  // era change: nothing enqueued earlier (on any stream) may still read the old keys, and every
+  // state derived from them is void -- the own share (its pk_me check was against the old keys)
+  // and the current epoch's prepared ciphertexts / verified shares
+  HIPCHK(c, hipDeviceSynchronize());
+  c->own_me = UINT32_MAX;
+  c->own_ready = false;
+  c->p_ct = 0;
+  c->ct_known = false;
+  c->n_shares = 0;
+  c->verified_p = 0;
+  c->coin_n = 0;
   if (!c->pk.ensure((size_t)n * sizeof(g1a)) || !c->pk_status.ensure((size_t)n * 4) ||
       !c->pk_comp.ensure((size_t)n * 48))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_pk_shares: out of device memory");
@@ -398,6 +436,8 @@ int hbx_set_own_share(hbx_ctx* c, uint32_t me, const uint8_t* sk32) {
     limbs[q] = ((uint32_t)sk32[31 - 4 * q - 3] << 24) | ((uint32_t)sk32[31 - 4 * q - 2] << 16) |
                ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
   if (!c->own_sk.ensure(32)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_own_share: out of device memory");
+  // a prepare enqueued earlier on any stream may still read own_sk
+  HIPCHK(c, hipDeviceSynchronize());
   HIPCHK(c, hipMemcpy(c->own_sk.p, limbs, 32, hipMemcpyHostToDevice));
   c->own_me = me;
   c->own_ready = false;
@@ -426,7 +466,7 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
       return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
     hipLaunchKernelGGL(k_prepare_ct, dim3(hash_blocks + dec_blocks), b64, 0, s, d_u_comp, d_v_blob, d_v_off,
                        d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
-                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr);
+                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->digest);
     c->own_ready = own;
   }
   HIPCHK(c, hipGetLastError());
@@ -446,6 +486,8 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   HIPCHK(c, hipGetLastError());
   c->p_ct = p;
   c->ct_known = false;
+  c->n_shares = 0;  // S / valid of an earlier verify belong to other ciphertexts
+  c->verified_p = 0;
   if (d_ct_valid) {
     // Ciphertext::verify now: one check per proposer (n = 0 share jobs, job 0 = the ciphertext)
     if (!c->S.ensure(sizeof(g1a)) || !c->S_status.ensure(4) || !c->valid.ensure(16))
@@ -530,6 +572,7 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
   HIPCHK(c, hipGetLastError());
   if (d_valid) HIPCHK(c, hipMemcpyAsync(d_valid, c->valid.p, m, hipMemcpyDeviceToDevice, s));
   c->n_shares = n;
+  c->verified_p = p;
   return HBX_OK;
 }
 
@@ -602,7 +645,35 @@ int hbx_merkle_validate_d(hbx_ctx* c, const uint8_t* d_values, uint32_t vlen, co
     return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_validate_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipLaunchKernelGGL(k_merkle_validate, dim3((nproofs + 63) / 64), dim3(64), 0, pick(c, stream), d_values, vlen,
-                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid);
+                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid, c->merkle);
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+uint32_t hbx_merkle_node_count(uint32_t n) { return n ? merkle_node_count(n) : 0; }
+
+int hbx_merkle_build_d(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* d_nodes,
+                       uint8_t* d_roots, void* stream) {
+  if (!c || !d_shards || !d_nodes || inst == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_build_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  uint8_t* roots = d_roots;
+  if (!roots) {
+    if (!c->roots.ensure((size_t)inst * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: roots");
+    roots = c->roots.as<uint8_t>();
+  }
+  return merkle_roots(c, d_shards, inst, n, L, roots, s, d_nodes);
+}
+
+int hbx_merkle_proofs_d(hbx_ctx* c, const uint8_t* d_nodes, uint32_t n, const uint32_t* d_req, uint32_t count,
+                        uint8_t* d_node_hash, uint8_t* d_sib_hash, uint32_t* d_sides, uint32_t* d_depth,
+                        uint8_t* d_root, void* stream) {
+  if (!c || !d_nodes || !d_req || !d_node_hash || !d_sib_hash || !d_sides || !d_depth || !d_root || count == 0 ||
+      n == 0 || n > (uint32_t)RS_MAX_N)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_proofs_d: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_merkle_proofs, dim3((count + 63) / 64), dim3(64), 0, pick(c, stream), d_nodes, n, d_req, count,
+                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -649,7 +720,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   {
     timed t_(c, HBX_K_HASH_NONCES, s);
     hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
-                       c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>());
+                       c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>(), c->digest);
   }
   HIPCHK(c, hipGetLastError());
   {
@@ -663,7 +734,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   }
   HIPCHK(c, hipGetLastError());
   if (h96) {
-    hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+    hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count, 1u,
                        c->coin_out96.as<uint8_t>());
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h96, c->coin_out96.p, (size_t)count * 96, hipMemcpyDeviceToHost, s));
@@ -782,7 +853,8 @@ int hbx_get_ct_valid_d(hbx_ctx* c, uint8_t* d_ct_valid, void* stream) {
 int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* d_status, void* stream) {
   if (!c || t == 0 || t > (uint32_t)COMBINE_MAX_T || !d_out_blob)
     return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt_d: bad args");
-  if (c->n_shares == 0 || c->p_ct == 0 || !c->ct_known) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares");
+  if (c->n_shares == 0 || c->p_ct == 0 || !c->ct_known || c->verified_p != c->p_ct)
+    return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares for the prepared ciphertexts");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   const uint32_t p = c->p_ct;
@@ -791,7 +863,8 @@ int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* 
   {
     timed t_(c, HBX_K_COMBINE, s);
     hipLaunchKernelGGL(k_combine, dim3(p), dim3(COMBINE_THREADS), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
-                       c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>());
+                       c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>(),
+                       c->digest);
   }
   HIPCHK(c, hipGetLastError());
   const uint64_t blocks = (c->max_v_len + 15) / 16;
@@ -843,6 +916,50 @@ int hbx_combine_decrypt(hbx_ctx* c, uint32_t t, uint8_t* out_blob, int32_t* stat
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (status) memcpy(status, st.data(), st.size() * 4);
   return HBX_OK;
+}
+
+// ---- status readout ---------------------------------------------------------------------------
+static int copy_status(hbx_ctx* c, const dbuf& b, size_t have, uint8_t* out, size_t count, const char* what) {
+  if (!out) return fail(c, HBX_E_INVALID_ARG, "%s: null output", what);
+  if (have == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "%s: nothing computed yet", what);
+  if (count != have) return fail(c, HBX_E_INVALID_ARG, "%s: count %zu, expected %zu", what, count, have);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());  // the last results may have been enqueued on any stream
+  HIPCHK(c, hipMemcpy(out, b.p, have, hipMemcpyDeviceToHost));
+  return HBX_OK;
+}
+
+int hbx_get_share_status(hbx_ctx* c, uint8_t* status, size_t count) {
+  if (!c) return HBX_E_INVALID_ARG;
+  return copy_status(c, c->valid, (size_t)c->n_shares * c->verified_p, status, count, "hbx_get_share_status");
+}
+
+int hbx_get_ct_status(hbx_ctx* c, uint8_t* status, size_t count) {
+  if (!c) return HBX_E_INVALID_ARG;
+  return copy_status(c, c->ct_valid, c->ct_known ? c->p_ct : 0, status, count, "hbx_get_ct_status");
+}
+
+int hbx_get_ct_hashes(hbx_ctx* c, uint8_t* h96, size_t count) {
+  if (!c || !h96) return fail(c, HBX_E_INVALID_ARG, "hbx_get_ct_hashes: bad args");
+  if (c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "hbx_get_ct_hashes: no ciphertexts prepared");
+  if (count != c->p_ct) return fail(c, HBX_E_INVALID_ARG, "hbx_get_ct_hashes: count %zu, expected %u", count, c->p_ct);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());
+  dbuf out;
+  if (!out.ensure(count * 96)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_get_ct_hashes: out of device memory");
+  hipLaunchKernelGGL(k_compress_g2, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, c->stream, c->G2pts.as<g2a>(),
+                     (uint32_t)count, 2u, out.as<uint8_t>());
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(h96, out.p, count * 96, hipMemcpyDeviceToHost);
+  out.release();
+  if (e != hipSuccess) return fail(c, HBX_E_DEVICE, "hbx_get_ct_hashes: %s", hipGetErrorString(e));
+  return HBX_OK;
+}
+
+int hbx_get_sig_share_status(hbx_ctx* c, uint8_t* status, size_t count) {
+  if (!c) return HBX_E_INVALID_ARG;
+  return copy_status(c, c->coin_valid, (size_t)c->coin_n * c->coin_I, status, count, "hbx_get_sig_share_status");
 }
 
 // ---- producer side --------------------------------------------------------------------------
@@ -917,7 +1034,8 @@ int hbx_encrypt(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, const 
   }
   if (ok) {
     hipLaunchKernelGGL(k_encrypt, dim3((p + 63) / 64), dim3(64), 0, c->stream, dpk.as<g1a>(), dr.as<uint8_t>(),
-                       dm.as<uint8_t>(), doff.as<uint64_t>(), p, du.as<uint8_t>(), dv.as<uint8_t>(), dw.as<uint8_t>());
+                       dm.as<uint8_t>(), doff.as<uint64_t>(), p, du.as<uint8_t>(), dv.as<uint8_t>(), dw.as<uint8_t>(),
+                       c->digest);
     ok = hipGetLastError() == hipSuccess &&
          hipMemcpyAsync(u48, du.p, (size_t)p * 48, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
          hipMemcpyAsync(w96, dw.p, (size_t)p * 96, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&

@@ -12,6 +12,7 @@
 // grid is (ceil(n/64), p) single-wave workgroups so all lanes of a wave share proposer j and
 // read its prepared lines at wave-uniform addresses.
 #include <hip/hip_runtime.h>
+#include "../../include/hbx.h"
 #include "hash.hpp"
 #include "pairing.hpp"
 #include "wide.hpp"
@@ -22,6 +23,18 @@ struct line_block {  // lines of one proposer: H then W
   line_pre h[MILLER_LINES];
   line_pre w[MILLER_LINES];
 };
+
+// Status of a share before its pairing check (include/hbx.h HBX_SHARE_*): HBX_SHARE_VALID means
+// "check it"; precedence follows what the reference would see first: no message, a message from
+// a non-validator (UnknownSender), a message serde cannot decode, a proposer whose ciphertext was
+// rejected (its shares are never verified).
+__device__ __forceinline__ uint8_t share_precheck(int32_t dec_status, bool present, bool known_sender, bool ct_ok) {
+  if (!present) return HBX_SHARE_ABSENT;
+  if (!known_sender) return HBX_SHARE_UNKNOWN_SENDER;
+  if (dec_status != HBX_PT_OK && dec_status != HBX_PT_INFINITY) return HBX_SHARE_UNDECODABLE;
+  if (!ct_ok) return HBX_SHARE_SKIPPED_CT;
+  return HBX_SHARE_VALID;
+}
 
 // e(PA, QA) * e(PB, QB) == 1 with identity handling (pairing with the identity is 1).
 __device__ __forceinline__ bool check2(const line_pre* LA, const g1a& PA, bool qa_inf,
@@ -69,7 +82,8 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    const uint8_t* __restrict__ w_comp, uint32_t p,
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
                                                    g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
-                                                   const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part) {
+                                                   const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part,
+                                                   int digest) {
   if (blockIdx.x >= hash_blocks) {
     // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2)
     const uint32_t k = (blockIdx.x - hash_blocks) * blockDim.x + threadIdx.x;
@@ -110,7 +124,7 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   const uint64_t off = v_off[j];
   const uint64_t len = v_off[j + 1] - off;
   uint8_t d[32];
-  hash_g1_g2_digest(u_comp + (size_t)j * 48, v_blob + off, len, d);
+  hash_g1_g2_digest(u_comp + (size_t)j * 48, v_blob + off, len, d, digest);
   g2j h;
   if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
 }
@@ -293,18 +307,17 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)j * n + i;
-  const int32_t st = s_status[idx];
-  const bool ok = (st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && ct_ok[j] &&
-                  (present == nullptr || present[idx] || i == me);
+  const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
+                                     ct_ok[j] != 0);
   bool v = false;
-  if (ok) {
+  if (res == HBX_SHARE_VALID) {
     g1a npk = pk[i];
     npk.y = fq_neg(npk.y);
     v = check2_lds(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf,
                    (lds_u32*)(gslots + threadIdx.x));
   }
-  valid[idx] = v ? 1 : 0;
-  if (i == me && ct_valid) ct_valid[j] = v ? 1 : 0;
+  valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+  if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
 }
 
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
@@ -336,7 +349,7 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
                                                              const g1a* __restrict__ S, uint32_t n,
                                                              uint32_t t, const uint8_t* __restrict__ ct_valid,
                                                              uint32_t* __restrict__ keys,
-                                                             int32_t* __restrict__ status) {
+                                                             int32_t* __restrict__ status, int digest) {
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;
   __shared__ g1j red[COMBINE_THREADS];
@@ -345,12 +358,12 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   if (tid == 0) {
     int c = 0;
     for (uint32_t i = 0; i < n && c < (int)t; i++)
-      if (valid[(size_t)j * n + i]) idx[c++] = (uint16_t)i;
+      if (valid[(size_t)j * n + i] == HBX_SHARE_VALID) idx[c++] = (uint16_t)i;
     s_count = c;
   }
   __syncthreads();
   const int count = s_count;
-  const bool ctv = ct_valid[j] != 0;
+  const bool ctv = ct_valid[j] == HBX_CT_VALID;
   if (!ctv || count < (int)t) {
     if (tid == 0) status[j] = !ctv ? -7 : -3;
     return;
@@ -378,7 +391,7 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
     const g1a g = g1_to_affine(red[0]);
     uint8_t comp[48], d[32];
     g1_compress(g, comp);
-    sha256_2(comp, 48, nullptr, 0, d);
+    digest2(digest, comp, 48, nullptr, 0, d);  // hash_bytes seed = DIGEST(compress(g))
     for (int q = 0; q < 8; q++)
       keys[(size_t)j * 8 + q] = ((uint32_t)d[4 * q] << 24) | ((uint32_t)d[4 * q + 1] << 16) |
                                 ((uint32_t)d[4 * q + 2] << 8) | d[4 * q + 3];
@@ -460,7 +473,7 @@ __global__ void __launch_bounds__(64) k_decrypt_shares(const uint8_t* __restrict
 __global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, const uint8_t* __restrict__ r32,
                                                 const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
                                                 uint32_t p, uint8_t* __restrict__ u48, uint8_t* __restrict__ v,
-                                                uint8_t* __restrict__ w96) {
+                                                uint8_t* __restrict__ w96, int digest) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p) return;
   uint32_t k[8];
@@ -471,12 +484,12 @@ __global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, cons
   g1_compress(u, uc);
   uint8_t gc[48], d[32];
   g1_compress(g, gc);
-  sha256_2(gc, 48, nullptr, 0, d);
+  digest2(digest, gc, 48, nullptr, 0, d);
   chacha_rng rng;
   chacha_rng_from_digest(rng, d);
   const uint64_t o = off[j], len = off[j + 1] - o;
   for (uint64_t q = 0; q < len; q++) v[o + q] = msg[o + q] ^ (uint8_t)chacha_next_u32(rng);
-  const g2j h = hash_g1_g2(uc, v + o, len);
+  const g2j h = hash_g1_g2(uc, v + o, len, digest);
   g2_compress(g2_to_affine(g2_mul_bits(h, k, 256)), w96 + (size_t)j * 96);
 }
 
@@ -588,7 +601,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
   const bool ok = ((bal >> ((tid & 63) & ~15)) & 0xFFFFull) == 0xFFFFull;
   if (lane == 0 && in_range) {
     const uint8_t res = (decodable && !needs_fallback && ok) ? 1 : 0;
-    if (ct_job) ct_valid[j] = res;
+    if (ct_job) ct_valid[j] = ct_ok[j] ? res : HBX_CT_UNDECODABLE;
     else valid[(size_t)j * n + q] = res;
     fallback[(size_t)j * (n + 1) + q] = needs_fallback ? JOB_FALLBACK : 0;
   }
@@ -642,13 +655,13 @@ __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict_
   else valid[(size_t)j * n + q] = v ? 1 : 0;
 }
 
-// valid[j][i] &= ct_valid[j]: the reference never verifies shares of a ciphertext that failed
-// Ciphertext::verify (honey_badger.rs:371-376).
+// Shares of a ciphertext that failed Ciphertext::verify become HBX_SHARE_SKIPPED_CT: the
+// reference never verifies them (honey_badger.rs:371-376), so they are neither valid nor a fault.
 __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid, const uint8_t* __restrict__ ct_valid,
                                                     uint32_t n, uint32_t p) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (size_t)n * p) return;
-  if (!ct_valid[k / n]) valid[k] = 0;
+  if (ct_valid[k / n] != HBX_CT_VALID && valid[k] <= HBX_SHARE_VALID) valid[k] = HBX_SHARE_SKIPPED_CT;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -657,11 +670,11 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
 // H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one HASH_K-lane
 // group each.
 __global__ void __launch_bounds__(64) k_hash_nonces(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
-                                                    uint32_t count, g2a* __restrict__ H) {
+                                                    uint32_t count, g2a* __restrict__ H, int digest) {
   const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / HASH_K;
   if (j >= count) return;  // whole groups only
   uint8_t d[32];
-  sha256_2(blob + off[j], off[j + 1] - off[j], nullptr, 0, d);
+  digest2(digest, blob + off[j], off[j + 1] - off[j], nullptr, 0, d);
   g2j h;
   if (hash_g2_group<HASH_K>(d, true, h)) H[j] = g2_to_affine(h);
 }
@@ -671,7 +684,12 @@ __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict_
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   g2a p;
-  status[i] = g2_decompress(comp + i * 96, p);
+  // decode = pairing 0.14's into_affine, as a SignatureShare is deserialised: on the curve AND in
+  // G2.  A share sig_i + T (T of cofactor order) could otherwise pass the ate check and carry T
+  // into the combined signature and its parity bit.
+  int32_t st = g2_decompress(comp + i * 96, p);
+  if (st == HBX_PT_OK && !g2_is_torsion_free(p)) st = HBX_PT_NOT_IN_SUBGROUP;
+  status[i] = st;
   out[i] = p;
 }
 
@@ -698,16 +716,16 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __rest
   const uint32_t inst = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)inst * n + i;
-  const int32_t st = sig_status[idx];
+  const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
   bool v = false;
-  if ((st == HBX_PT_OK || st == HBX_PT_INFINITY) && i < n_keys && (present == nullptr || present[idx])) {
+  if (res == HBX_SHARE_VALID) {
     g1a ng;
     ng.x = fq_from_const(G1_GEN_X);
     ng.y = fq_neg(fq_from_const(G1_GEN_Y));
     ng.inf = false;
     v = check_mixed(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng);
   }
-  valid[idx] = v ? 1 : 0;
+  valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
 }
 
 // B3: PublicKeySet::combine_signatures over the first t valid shares in node-index order
@@ -725,7 +743,7 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
   if (tid == 0) {
     int c = 0;
     for (uint32_t i = 0; i < n && c < (int)t; i++)
-      if (valid[(size_t)inst * n + i]) idx[c++] = (uint16_t)i;
+      if (valid[(size_t)inst * n + i] == HBX_SHARE_VALID) idx[c++] = (uint16_t)i;
     s_count = c;
   }
   __syncthreads();
@@ -782,10 +800,11 @@ __global__ void __launch_bounds__(64) k_master_verify(const line_pre* __restrict
   g2_compress(s, sig96 + (size_t)j * 96);
 }
 
-__global__ void __launch_bounds__(64) k_compress_g2(const g2a* __restrict__ pts, uint32_t count,
+// compressed encodings of pts[j * stride], j < count
+__global__ void __launch_bounds__(64) k_compress_g2(const g2a* __restrict__ pts, uint32_t count, uint32_t stride,
                                                     uint8_t* __restrict__ out96) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < count) g2_compress(pts[j], out96 + (size_t)j * 96);
+  if (j < count) g2_compress(pts[(size_t)j * stride], out96 + (size_t)j * 96);
 }
 
 // SecretKeyShare::sign (common_coin.rs:142): sig[inst][i] = sk_i * H_inst, compressed.

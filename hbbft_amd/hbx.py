@@ -58,7 +58,32 @@ EXPORTS = (
     "hbx_broadcast_decode_d",
     "hbx_set_timing",
     "hbx_kernel_time",
+    "hbx_get_share_status",
+    "hbx_get_ct_status",
+    "hbx_get_sig_share_status",
+    "hbx_get_ct_hashes",
+    "hbx_set_digest",
+    "hbx_set_merkle_digest",
+    "hbx_merkle_node_count",
+    "hbx_merkle_build_d",
+    "hbx_merkle_proofs_d",
 )
+
+DIGEST_SHA256 = 0
+DIGEST_SHA3_256 = 1
+MERKLE_SHA256 = 0
+MERKLE_SHA3 = 1
+
+# Per-share / per-ciphertext status bytes (include/hbx.h HBX_SHARE_*, HBX_CT_*)
+SHARE_INVALID = 0
+SHARE_VALID = 1
+SHARE_ABSENT = 2
+SHARE_UNDECODABLE = 3
+SHARE_SKIPPED_CT = 4
+SHARE_UNKNOWN_SENDER = 5
+CT_INVALID = 0
+CT_VALID = 1
+CT_UNDECODABLE = 3
 
 # kernel ids of hbx_kernel_time (include/hbx.h)
 KERNELS = {"prepare_ct": 0, "prepare_lines": 1, "ct_checks": 2, "verify_shares": 3, "combine": 4,
@@ -115,6 +140,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
     lib.hbx_set_timing.argtypes = [P, ctypes.c_int]
     lib.hbx_kernel_time.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+    lib.hbx_set_digest.argtypes = [P, ctypes.c_int]
+    lib.hbx_set_merkle_digest.argtypes = [P, ctypes.c_int]
+    lib.hbx_merkle_node_count.argtypes = [u32]
+    lib.hbx_merkle_node_count.restype = u32
+    lib.hbx_merkle_build_d.argtypes = [P, P, u32, u32, u32, P, P, P]
+    lib.hbx_merkle_proofs_d.argtypes = [P, P, u32, P, u32, P, P, P, P, P, P]
+    for name in ("hbx_get_share_status", "hbx_get_ct_status", "hbx_get_sig_share_status", "hbx_get_ct_hashes"):
+        getattr(lib, name).argtypes = [P, u8p, ctypes.c_size_t]
     _lib = lib
     return lib
 
@@ -164,6 +197,14 @@ class Context:
     def _check(self, rc: int):
         if rc != HBX_OK:
             raise HbxError(rc, self.lib.hbx_last_error(self.h).decode())
+
+    def set_digest(self, variant: int):
+        """hbx_set_digest: DIGEST_SHA256 (default) or DIGEST_SHA3_256 for hash_g2 / hash_g1_g2 / hash_bytes."""
+        self._check(self.lib.hbx_set_digest(self.h, variant))
+
+    def set_merkle_digest(self, variant: int):
+        """hbx_set_merkle_digest: MERKLE_SHA256 (default, afck merkle) or MERKLE_SHA3."""
+        self._check(self.lib.hbx_set_merkle_digest(self.h, variant))
 
     # -- instrumentation -----------------------------------------------------------------------
     def set_timing(self, on: bool = True):
@@ -221,6 +262,30 @@ class Context:
             res.append(out[int(off[j]):int(off[j + 1])].tobytes() if st[j] == HBX_OK else None)
         return res, st
 
+    def share_status(self, p: int, n: int) -> np.ndarray:
+        """HBX_SHARE_* byte of every share of the last verification -> uint8[p, n]."""
+        out = np.zeros(p * n, dtype=np.uint8)
+        self._check(self.lib.hbx_get_share_status(self.h, _u8(out), out.size))
+        return out.reshape(p, n)
+
+    def ct_status(self, p: int) -> np.ndarray:
+        """HBX_CT_* byte of every prepared ciphertext -> uint8[p]."""
+        out = np.zeros(p, dtype=np.uint8)
+        self._check(self.lib.hbx_get_ct_status(self.h, _u8(out), out.size))
+        return out
+
+    def ct_hashes(self, p: int) -> np.ndarray:
+        """Compressed H_j = hash_g1_g2(U_j, V_j) of the prepared ciphertexts -> uint8[p, 96]."""
+        out = np.zeros(p * 96, dtype=np.uint8)
+        self._check(self.lib.hbx_get_ct_hashes(self.h, _u8(out), p))
+        return out.reshape(p, 96)
+
+    def sig_share_status(self, count: int, n: int) -> np.ndarray:
+        """HBX_SHARE_* byte of every signature share of the last hbx_verify_sig_shares."""
+        out = np.zeros(count * n, dtype=np.uint8)
+        self._check(self.lib.hbx_get_sig_share_status(self.h, _u8(out), out.size))
+        return out.reshape(count, n)
+
     # -- producer side (SURVEY.md §8(a) A6) -------------------------------------------------------
     def public_keys(self, sk32: np.ndarray) -> np.ndarray:
         """sk32: uint8[n, 32] big-endian canonical scalars -> uint8[n, 48] compressed g1 * sk."""
@@ -264,15 +329,25 @@ class Context:
         self._check(self.lib.hbx_set_own_share(self.h, me, _u8(sk)))
 
     # -- device API (torch tensors as HBM buffers; torch is plumbing only) -----------------------
+    # stream=None enqueues on torch's current stream of the context's device (the C ABI's NULL is
+    # the HIP null stream, which is what torch's default stream is), so the calls are ordered
+    # with the tensor uploads and reads the caller did on that stream.
+    def _stream(self, stream):
+        if stream is not None:
+            return stream
+        import torch
+
+        return torch.cuda.current_stream(self.device).cuda_stream
+
     def prepare_ciphertexts_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_ct_valid=None, stream=None):
         self._check(self.lib.hbx_prepare_ciphertexts_d(
             self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
-            None if d_ct_valid is None else d_ct_valid.data_ptr(), stream))
+            None if d_ct_valid is None else d_ct_valid.data_ptr(), self._stream(stream)))
 
     def verify_dec_shares_d(self, d_shares, n: int, p: int, d_valid=None, d_present=None, stream=None):
         self._check(self.lib.hbx_verify_dec_shares_d(
             self.h, d_shares.data_ptr(), None if d_present is None else d_present.data_ptr(), n, p,
-            None if d_valid is None else d_valid.data_ptr(), stream))
+            None if d_valid is None else d_valid.data_ptr(), self._stream(stream)))
 
     # -- common coin ------------------------------------------------------------------------------
     def prepare_nonces(self, nonces: Sequence[bytes]) -> np.ndarray:
@@ -322,43 +397,57 @@ class Context:
         """d_shards: uint8[inst, k + m, L] (parity rows overwritten)."""
         inst, n, L = d_shards.shape
         assert n == k + m
-        self._check(self.lib.hbx_rs_encode_d(self.h, d_shards.data_ptr(), inst, k, m, L, stream))
+        self._check(self.lib.hbx_rs_encode_d(self.h, d_shards.data_ptr(), inst, k, m, L, self._stream(stream)))
 
     def rs_reconstruct_d(self, d_shards, d_present, d_status, k: int, m: int, stream=None):
         inst, n, L = d_shards.shape
         self._check(self.lib.hbx_rs_reconstruct_d(self.h, d_shards.data_ptr(), d_present.data_ptr(), inst, k, m, L,
-                                                  d_status.data_ptr(), stream))
+                                                  d_status.data_ptr(), self._stream(stream)))
 
     def merkle_roots_d(self, d_shards, d_roots, stream=None):
         inst, n, L = d_shards.shape
-        self._check(self.lib.hbx_merkle_roots_d(self.h, d_shards.data_ptr(), inst, n, L, d_roots.data_ptr(), stream))
+        self._check(self.lib.hbx_merkle_roots_d(self.h, d_shards.data_ptr(), inst, n, L, d_roots.data_ptr(), self._stream(stream)))
 
     def merkle_validate_d(self, d_values, d_nodes, d_sibs, d_sides, d_depth, d_root, d_sender, count: int, d_valid,
                           stream=None):
         nproofs, vlen = d_values.shape
         self._check(self.lib.hbx_merkle_validate_d(
             self.h, d_values.data_ptr(), vlen, d_nodes.data_ptr(), d_sibs.data_ptr(), d_sides.data_ptr(),
-            d_depth.data_ptr(), d_root.data_ptr(), d_sender.data_ptr(), count, nproofs, d_valid.data_ptr(), stream))
+            d_depth.data_ptr(), d_root.data_ptr(), d_sender.data_ptr(), count, nproofs, d_valid.data_ptr(), self._stream(stream)))
+
+    def merkle_node_count(self, n: int) -> int:
+        return int(self.lib.hbx_merkle_node_count(n))
+
+    def merkle_build_d(self, d_shards, d_nodes, d_roots=None, stream=None):
+        inst, n, L = d_shards.shape
+        self._check(self.lib.hbx_merkle_build_d(self.h, d_shards.data_ptr(), inst, n, L, d_nodes.data_ptr(),
+                                                None if d_roots is None else d_roots.data_ptr(), self._stream(stream)))
+
+    def merkle_proofs_d(self, d_nodes, n: int, d_req, d_node_hash, d_sib_hash, d_sides, d_depth, d_root, stream=None):
+        count = d_req.shape[0]
+        self._check(self.lib.hbx_merkle_proofs_d(self.h, d_nodes.data_ptr(), n, d_req.data_ptr(), count,
+                                                 d_node_hash.data_ptr(), d_sib_hash.data_ptr(), d_sides.data_ptr(),
+                                                 d_depth.data_ptr(), d_root.data_ptr(), self._stream(stream)))
 
     def broadcast_decode_d(self, d_shards, d_present, d_root, k: int, m: int, d_out, d_out_len, d_status, stream=None):
         inst, n, L = d_shards.shape
         self._check(self.lib.hbx_broadcast_decode_d(
             self.h, d_shards.data_ptr(), d_present.data_ptr(), d_root.data_ptr(), inst, k, m, L, d_out.data_ptr(),
-            d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), stream))
+            d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), self._stream(stream)))
 
     def get_ct_valid_d(self, d_ct_valid, stream=None):
-        self._check(self.lib.hbx_get_ct_valid_d(self.h, d_ct_valid.data_ptr(), stream))
+        self._check(self.lib.hbx_get_ct_valid_d(self.h, d_ct_valid.data_ptr(), self._stream(stream)))
 
     def combine_decrypt_d(self, t: int, d_out, d_status=None, stream=None):
         self._check(self.lib.hbx_combine_decrypt_d(
-            self.h, t, d_out.data_ptr(), None if d_status is None else d_status.data_ptr(), stream))
+            self.h, t, d_out.data_ptr(), None if d_status is None else d_status.data_ptr(), self._stream(stream)))
 
     def decrypt_epoch_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_shares, n: int, t: int, d_out,
                         d_valid=None, d_ct_valid=None, d_status=None, d_present=None, stream=None):
-        """One node-epoch (hbx_decrypt_epoch_d): prepare + share checks + Ciphertext::verify beside the
-        speculative combine + decrypt; same results as the three-call sequence."""
+        """One node-epoch (hbx_decrypt_epoch_d): prepare + share checks (with Ciphertext::verify) +
+        combine + decrypt; same results as the three-call sequence."""
         opt = lambda x: None if x is None else x.data_ptr()  # noqa: E731
         self._check(self.lib.hbx_decrypt_epoch_d(
             self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
             d_shares.data_ptr(), opt(d_present), n, t, opt(d_valid), opt(d_ct_valid), d_out.data_ptr(),
-            opt(d_status), stream))
+            opt(d_status), self._stream(stream)))

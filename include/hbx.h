@@ -9,8 +9,9 @@
  *  - Functions without the `_d` suffix take HOST pointers, stage through device buffers owned
  *    by the context and block until results are back on the host.
  *  - Functions with the `_d` suffix take DEVICE pointers (hipMalloc'd on the context's device)
- *    and a hipStream_t passed as `void*` (NULL = the context's own stream); they enqueue work
- *    and return without synchronising.
+ *    and a hipStream_t passed as `void*` (NULL = the HIP null stream, i.e. what a framework's
+ *    default stream hands over); they enqueue work on that stream, in stream order with the
+ *    caller's own work on it, and return without synchronising.
  *  - Return value: HBX_OK (0) or a negative HBX_E_* code.  A failed verification is NOT an error:
  *    it is a 0 in the corresponding validity output, exactly as the reference returns `false`.
  *  - Validity outputs are byte-per-item (1 = valid) in the `_d` API and little-endian bitmaps
@@ -52,6 +53,48 @@ extern "C" {
 #define HBX_PT_INFINITY 4
 #define HBX_PT_NOT_IN_SUBGROUP 5 /* on the curve but not in G1 / G2 (pairing's into_affine rejects it) */
 
+/* Per-share status (one byte per share: the d_valid arrays of the _d API, hbx_get_share_status,
+ * hbx_get_sig_share_status).  1 = valid and 0 = verified false, so "byte == 1" is "valid";
+ * the other codes tell the caller which reference fault, if any, the share maps to:
+ *   HBX_SHARE_INVALID        verify returned false: FaultKind::UnverifiedDecryptionShareSender
+ *                            (honey_badger.rs:199, :437) / UnverifiedSignatureShareSender
+ *                            (common_coin.rs:153); the share is dropped.
+ *   HBX_SHARE_VALID          verified true.
+ *   HBX_SHARE_ABSENT         present bit 0: no message, nothing to report.
+ *   HBX_SHARE_UNDECODABLE    the 48/96 bytes are not a subgroup point: the reference never sees
+ *                            such a share (serde/bincode rejects the message before
+ *                            HoneyBadger/CommonCoin), so no fault kind of the algorithm applies.
+ *   HBX_SHARE_SKIPPED_CT     not verified because the proposer's ciphertext failed to decode or
+ *                            Ciphertext::verify: the reference skips that proposer
+ *                            (honey_badger.rs:359-376) and never verifies its shares.
+ *   HBX_SHARE_UNKNOWN_SENDER sender index >= n of hbx_set_pk_shares: the reference rejects the
+ *                            message with Error UnknownSender (honey_badger.rs:64-66,
+ *                            common_coin.rs:158).  (own-share mode: `me` is always checked.) */
+#define HBX_SHARE_INVALID 0
+#define HBX_SHARE_VALID 1
+#define HBX_SHARE_ABSENT 2
+#define HBX_SHARE_UNDECODABLE 3
+#define HBX_SHARE_SKIPPED_CT 4
+#define HBX_SHARE_UNKNOWN_SENDER 5
+
+/* Per-ciphertext status (d_ct_valid of the _d API, hbx_get_ct_status):
+ *   HBX_CT_INVALID      Ciphertext::verify returned false: FaultKind::ShareDecryptionFailed
+ *                       (honey_badger.rs:371-375).
+ *   HBX_CT_VALID        verified.
+ *   HBX_CT_UNDECODABLE  U or W does not decode to a subgroup point: bincode::deserialize of the
+ *                       ciphertext fails, FaultKind::InvalidCiphertext (honey_badger.rs:359-368). */
+#define HBX_CT_INVALID 0
+#define HBX_CT_VALID 1
+#define HBX_CT_UNDECODABLE 3
+
+/* Digest variants (hbx_set_digest, hbx_set_merkle_digest). */
+#define HBX_DIGEST_SHA256 0   /* default: ring SHA-256 (reference Cargo.toml:32) */
+#define HBX_DIGEST_SHA3_256 1 /* tiny-keccak SHA3-256 */
+#define HBX_MERKLE_SHA256 0   /* default: merkle (afck fork) + ring SHA-256, leaf H(0x00||v),
+                                 node H(0x01||l||r), odd node promoted (broadcast.rs:161, :381) */
+#define HBX_MERKLE_SHA3 1     /* later hbbft's own tree (src/broadcast/merkle.rs, tiny-keccak):
+                                 leaf SHA3(v), node SHA3(l||r), odd node promoted */
+
 typedef struct hbx_ctx hbx_ctx;
 
 /* Create / destroy a context bound to HIP device `device`. */
@@ -81,12 +124,25 @@ int hbx_set_timing(hbx_ctx* ctx, int on);
 int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launches);
 
 /* ---------------------------------------------------------------------------------------------
+ * DIGEST of threshold_crypto's hash_g2 / hash_g1_g2 / hash_bytes.  The
+ * reference's threshold_crypto dependency is an unpinned git revision (Cargo.toml:35): revisions
+ * hash with SHA-256 or with tiny-keccak's SHA3-256.  Per context, default HBX_DIGEST_SHA256;
+ * switching voids the prepared ciphertexts / nonces.  Affects every H_j, W, plaintext keystream,
+ * nonce hash and signature of this context.
+ * hbx_set_merkle_digest -- the Merkle tree of the broadcast calls (HBX_MERKLE_*).
+ * ------------------------------------------------------------------------------------------- */
+int hbx_set_digest(hbx_ctx* ctx, int variant);
+int hbx_set_merkle_digest(hbx_ctx* ctx, int variant);
+
+/* ---------------------------------------------------------------------------------------------
  * Key material (once per era).
  * Replaces: NetworkInfo::new's public_key_share derivation (src/messaging.rs:251-254) and the
  * per-call lookup NetworkInfo::public_key_share (src/messaging.rs:312) used by
  * HoneyBadger::verify_decryption_share (src/honey_badger/honey_badger.rs:228-232).
  * pk_comp: n x 48 B compressed pk_i (node index order = BTreeMap order, messaging.rs:246-250).
  * status (optional, n entries): HBX_PT_* per key.
+ * A new key set clears this node's own share (hbx_set_own_share must be called again for the
+ * new era) and every epoch result computed under the old keys.
  * ------------------------------------------------------------------------------------------- */
 int hbx_set_pk_shares(hbx_ctx* ctx, const uint8_t* pk_comp, uint32_t n, int32_t* status);
 
@@ -122,12 +178,23 @@ int hbx_prepare_ciphertexts(hbx_ctx* ctx, const uint8_t* u_comp, const uint8_t* 
  * Replaces: PublicKeyShare::verify_decryption_share (src/honey_badger/honey_badger.rs:229) as
  * called from verify_pending_decryption_shares (:422-444) and handle_decryption_share_message
  * (:198).  valid[j][i] = e(S_ji, H_j) == e(pk_i, W_j).  Absent shares (present bit 0), unknown
- * senders (i >= n of hbx_set_pk_shares) and undecodable encodings give 0.
+ * senders (i >= n of hbx_set_pk_shares), undecodable encodings and shares of a ciphertext that
+ * failed hbx_prepare_ciphertexts give 0; hbx_get_share_status tells these apart (HBX_SHARE_*),
+ * so a caller raises UnverifiedDecryptionShareSender exactly for HBX_SHARE_INVALID.
  * shares: p x n x 48 B; present_bits: ceil(p*n/8) B (NULL = all present);
  * valid_bits: ceil(p*n/8) B out (bit j*n + i).
  * ------------------------------------------------------------------------------------------- */
 int hbx_verify_dec_shares(hbx_ctx* ctx, const uint8_t* shares, const uint8_t* present_bits,
                           uint32_t n, uint32_t p, uint8_t* valid_bits);
+
+/* Status bytes of the last share verification (p x n, HBX_SHARE_*) and of the last prepared
+ * ciphertexts (p, HBX_CT_*), copied to the host (blocking).  count must equal p*n (resp. p). */
+int hbx_get_share_status(hbx_ctx* ctx, uint8_t* status, size_t count);
+int hbx_get_ct_status(hbx_ctx* ctx, uint8_t* status, size_t count);
+/* The hoisted H_j = hash_g1_g2(U_j, V_j) of the last prepared ciphertexts (threshold_crypto,
+ * recomputed by the reference inside every verify_decryption_share, honey_badger.rs:229),
+ * compressed, p x 96 B; the identity for a ciphertext that does not decode. */
+int hbx_get_ct_hashes(hbx_ctx* ctx, uint8_t* h96, size_t count);
 
 /* ---------------------------------------------------------------------------------------------
  * Threshold decryption of every proposer's contribution.
@@ -142,7 +209,10 @@ int hbx_combine_decrypt(hbx_ctx* ctx, uint32_t t, uint8_t* out_blob, int32_t* st
 
 /* ---------------------------------------------------------------------------------------------
  * Device-pointer / stream variants (inputs resident in HBM; nothing is copied to the host).
- *   d_valid / d_ct_valid / d_present are byte-per-item arrays.
+ *   d_present is a byte-per-share array (nonzero = present); d_valid receives one HBX_SHARE_*
+ *   status byte per share and d_ct_valid one HBX_CT_* byte per ciphertext (1 = valid in both).
+ *   A prepare invalidates the previous verification: combine needs a verify of the same p after
+ *   the latest prepare (HBX_E_NO_CIPHERTEXTS otherwise).
  * hbx_prepare_ciphertexts_d with d_ct_valid == NULL DEFERS Ciphertext::verify: the checks then run
  * fused into the next hbx_verify_dec_shares_d launch (one more pairing check per proposer next
  * to its n share checks), and hbx_get_ct_valid_d copies the result out afterwards.
@@ -203,6 +273,8 @@ int hbx_prepare_nonces(hbx_ctx* ctx, const uint8_t* nonce_blob, const uint64_t* 
 int hbx_sign(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, uint8_t* sig96);
 int hbx_verify_sig_shares(hbx_ctx* ctx, const uint8_t* sig96, const uint8_t* present_bits, uint32_t n,
                           uint32_t count, uint8_t* valid_bits);
+/* HBX_SHARE_* status of every share of the last hbx_verify_sig_shares (count x n bytes). */
+int hbx_get_sig_share_status(hbx_ctx* ctx, uint8_t* status, size_t count);
 int hbx_combine_signatures(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96,
                            int32_t* status, uint8_t* master_ok_bits, uint8_t* parity_bits);
 
@@ -241,6 +313,21 @@ int hbx_merkle_validate_d(hbx_ctx* ctx, const uint8_t* d_values, uint32_t vlen, 
                           const uint8_t* d_sib_hash, const uint32_t* d_sides, const uint32_t* d_depth,
                           const uint8_t* d_root, const uint32_t* d_sender, uint32_t count, uint32_t nproofs,
                           uint8_t* d_valid, void* stream);
+/* hbx_merkle_build_d -- MerkleTree::from_vec over the index-prefixed shards, keeping the whole
+ *   tree (SURVEY.md §8(b) hbx_merkle_build): d_nodes[inst][hbx_merkle_node_count(n)][32], the
+ *   levels from the n leaf digests up to the root (last), a promoted odd node repeated on the
+ *   level it moves to; d_roots[inst][32] optional.
+ * hbx_merkle_proofs_d -- MerkleTree::gen_proof (src/broadcast.rs:389-401: one Value proof per
+ *   node) from such trees: proof q for leaf d_req[2q + 1] of instance d_req[2q] (the proof of the
+ *   first leaf with an equal digest, as merkle.rs finds the first equal value), written in the
+ *   format hbx_merkle_validate_d reads (d_node_hash[q][17][32] root first, d_sib_hash[q][16][32],
+ *   d_sides[q], d_depth[q], d_root[q][32]). */
+uint32_t hbx_merkle_node_count(uint32_t n);
+int hbx_merkle_build_d(hbx_ctx* ctx, const uint8_t* d_shards, uint32_t inst, uint32_t n, uint32_t L,
+                       uint8_t* d_nodes, uint8_t* d_roots, void* stream);
+int hbx_merkle_proofs_d(hbx_ctx* ctx, const uint8_t* d_nodes, uint32_t n, const uint32_t* d_req, uint32_t count,
+                        uint8_t* d_node_hash, uint8_t* d_sib_hash, uint32_t* d_sides, uint32_t* d_depth,
+                        uint8_t* d_root, void* stream);
 int hbx_broadcast_decode_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t* d_present,
                            const uint8_t* d_root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
                            uint8_t* d_out, uint64_t out_stride, uint64_t* d_out_len, int32_t* d_status,

@@ -1,0 +1,168 @@
+"""HoneyBadger's threshold-decryption sub-path, one message at a time -- TEST ORACLE ONLY.
+
+Only ``tests/`` (and fixture scripts under ``tests/golden/``) may import this.  It restates what
+``src/honey_badger/honey_badger.rs`` does for ONE epoch on ONE node, line by line, with the CPU
+crypto of ``oracle/threshold.py``, so that the batched replay in ``hbbft_amd/honey_badger.py`` (one
+engine call for the whole epoch) can be checked to emit the same FaultLog, in the same order, and
+the same Batch:
+
+* ``handle_decryption_share_message``  honey_badger.rs:186-217 -- verify at once if the proposer's
+  ciphertext is known (fault ``UnverifiedDecryptionShareSender`` and drop, :198-201), else store
+  unverified; insert (BTreeMap: a later share of the same sender replaces the earlier one);
+  ``try_output_batches``;
+* ``send_decryption_shares``           :351-391 -- per proposer in BTreeMap order: bincode
+  failure -> ``InvalidCiphertext`` (:359-368), ``!ciphertext.verify()`` -> ``ShareDecryptionFailed``
+  (:371-375), both ``continue`` before any share of that proposer is verified;
+  ``verify_pending_decryption_shares`` (:422-444, senders in BTreeMap order) +
+  ``remove_incorrect_decryption_shares`` (:446-461); own share ``decrypt_share_no_verify``
+  inserted unverified (:394-418); then ``try_output_batches``;
+* ``try_output_batch`` / ``try_decrypt_proposer_contribution`` :237-283, :315-349 -- ``all()``
+  over the proposers with a ciphertext (short-circuit kept), ``> f`` shares needed (:328),
+  ``PublicKeySet::decrypt`` over the shares present at that moment (first t by index); a decrypt
+  error is only logged (:345) and that proposer is left out of the batch; after the batch the
+  epoch advances, so later messages of this epoch are ignored (handle_message :68-76).
+
+Message model (what crosses the wire in the reference):
+  ("share", sender, proposer, share48)  -- a DecryptionShare message.  ``share48`` that is not a
+                                           G1 subgroup point is rejected by serde before
+                                           HoneyBadger sees it: no fault, no state change.
+                                           A sender >= n is not a validator: ``handle_message``
+                                           returns ``Err(UnknownSender)`` (:64-66), recorded in
+                                           ``errors``.
+  ("acs", {proposer: (u48, v, w96)})    -- the CommonSubset output (the accepted ciphertexts).
+Node indices are the BTreeMap order of the node ids (messaging.rs:246-250).
+"""
+from __future__ import annotations
+
+from . import bls12_381 as bls
+from . import threshold as tc
+
+UNVERIFIED_DECRYPTION_SHARE_SENDER = "UnverifiedDecryptionShareSender"
+INVALID_CIPHERTEXT = "InvalidCiphertext"
+SHARE_DECRYPTION_FAILED = "ShareDecryptionFailed"
+UNKNOWN_SENDER = "UnknownSender"
+
+
+def decode_share(b: bytes):
+    """DecryptionShare deserialisation (pairing 0.14 into_affine: curve + subgroup); None if it
+    fails, ("ok", point) otherwise (the point may be the identity)."""
+    try:
+        return ("ok", bls.g1_decompress(bytes(b)))
+    except ValueError:
+        return None
+
+
+def decode_ciphertext(ct):
+    """bincode::deserialize::<Ciphertext> of (u48, v, w96): None on a malformed point."""
+    u48, v, w96 = ct
+    try:
+        return (bls.g1_decompress(bytes(u48)), bytes(v), bls.g2_decompress(bytes(w96)))
+    except ValueError:
+        return None
+
+
+class EpochNode:
+    """One node's view of one HoneyBadger epoch (decryption sub-path only)."""
+
+    def __init__(self, n: int, our_index: int, pk_set: tc.PublicKeySet, sk_share: int, variant: str = tc.DEFAULT_DIGEST):
+        self.n = n
+        self.f = (n - 1) // 3  # NetworkInfo::num_faulty, messaging.rs:258
+        self.me = our_index
+        self.pk_set = pk_set
+        self.pk_shares = [pk_set.public_key_share(i) for i in range(n)]
+        self.sk = sk_share
+        self.variant = variant
+        self.ciphertexts = None  # proposer -> decoded ciphertext, once the ACS output is in
+        self.hashes = {}  # hash_g1_g2 per proposer (cached: a pure function of the ciphertext)
+        self.received = {}  # proposer -> {sender: share point}
+        self.decrypted = {}  # proposer -> plaintext bytes
+        self.decrypt_errors = []  # proposers whose PublicKeySet::decrypt failed (:345)
+        self.faults = []  # (node index, FaultKind name), in emission order
+        self.errors = []  # (node index, error name): handle_message returned Err
+        self.batch = None  # proposer -> plaintext, once output
+        self.done = False  # the epoch advanced (later messages of it are ignored)
+
+    # -- crypto ---------------------------------------------------------------------------------
+    def _verify_share(self, sender: int, share, proposer: int, ct) -> bool:
+        """HoneyBadger::verify_decryption_share (:222-233)."""
+        if sender >= self.n:
+            return False
+        return tc.verify_decryption_share(self.pk_shares[sender], share, ct, self.variant, hash_pt=self.hashes[proposer])
+
+    # -- message handlers -------------------------------------------------------------------------
+    def handle(self, event):
+        if self.done:
+            return  # a message of a past epoch: ignored (:68-76)
+        if event[0] == "share":
+            _, sender, proposer, share48 = event
+            if sender >= self.n:
+                self.errors.append((sender, UNKNOWN_SENDER))
+                return
+            dec = decode_share(share48)
+            if dec is None:
+                return  # never reaches HoneyBadger
+            self._handle_decryption_share(sender, proposer, dec[1])
+        elif event[0] == "acs":
+            self._send_decryption_shares(event[1])
+        else:
+            raise ValueError(event[0])
+
+    def _handle_decryption_share(self, sender: int, proposer: int, share):
+        if self.ciphertexts is not None and proposer in self.ciphertexts:
+            if not self._verify_share(sender, share, proposer, self.ciphertexts[proposer]):
+                self.faults.append((sender, UNVERIFIED_DECRYPTION_SHARE_SENDER))
+                return
+        self.received.setdefault(proposer, {})[sender] = share
+        self._try_output_batches()
+
+    def _send_decryption_shares(self, cs_output):
+        cts = {}
+        for proposer in sorted(cs_output):
+            ct = decode_ciphertext(cs_output[proposer])
+            if ct is None:
+                self.faults.append((proposer, INVALID_CIPHERTEXT))
+                continue
+            h = tc.hash_g1_g2(ct[0], ct[1], self.variant)
+            if not tc.ciphertext_verify(ct, self.variant, hash_pt=h):
+                self.faults.append((proposer, SHARE_DECRYPTION_FAILED))
+                continue
+            self.hashes[proposer] = h
+            # verify_pending_decryption_shares + remove_incorrect_decryption_shares
+            pending = self.received.get(proposer, {})
+            incorrect = [s for s in sorted(pending) if not self._verify_share(s, pending[s], proposer, ct)]
+            for s in incorrect:
+                self.faults.append((s, UNVERIFIED_DECRYPTION_SHARE_SENDER))
+                del pending[s]
+            # send_decryption_share: our own share, inserted unverified
+            self.received.setdefault(proposer, {})[self.me] = tc.decrypt_share(self.sk, ct)
+            cts[proposer] = ct
+        self.ciphertexts = cts
+        self._try_output_batches()
+
+    # -- output -----------------------------------------------------------------------------------
+    def _try_decrypt(self, proposer: int) -> bool:
+        if proposer in self.decrypted or proposer in self.decrypt_errors:
+            return True
+        shares = self.received.get(proposer)
+        if not shares:
+            return False
+        if len(shares) <= self.f:
+            return False
+        ct = self.ciphertexts[proposer]
+        try:
+            self.decrypted[proposer] = tc.decrypt(self.pk_set, sorted(shares.items()), ct, self.variant)
+        except (tc.NotEnoughShares, tc.DuplicateEntry):
+            self.decrypt_errors.append(proposer)
+        return True
+
+    def _try_output_batches(self):
+        if self.done or self.ciphertexts is None:
+            return
+        if all(self._try_decrypt(pid) for pid in sorted(self.ciphertexts)):
+            self.batch = dict(self.decrypted)
+            self.done = True
+
+    def run(self, events):
+        for ev in events:
+            self.handle(ev)
+        return self

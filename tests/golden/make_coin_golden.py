@@ -1,17 +1,21 @@
-"""Generate the committed Common Coin fixture (tests/golden/coin_n{4,7}.npz) with the oracle.
+"""Generate the committed Common Coin fixtures with the oracle.
 
-    python tests/golden/make_coin_golden.py
+    python tests/golden/make_coin_golden.py      # coin_n4, coin_n7 (edge cases), coin_n128 (config 4)
 
 One node's view of `count` concurrent coin instances (SURVEY.md §3 stack B): nonces formatted as
 Nonce::new(invocation_id = master public key bytes, session, proposer, agreement_epoch = 2)
 (src/agreement/mod.rs:155-165, messaging.rs:342-344), signature shares sig_i = sk_i * hash_g2(nonce)
 (common_coin.rs:142), with faults: a share over a DIFFERENT nonce (valid signature, wrong message),
-an undecodable encoding, an absent share, and one instance left with fewer than t shares
-(NotEnoughShares).  Expected: validity bits (common_coin.rs:151), combined signature of the first
-t valid shares in index order (:190), master verification (:196), parity (:173).
+an undecodable encoding, an honest share plus a point of the cofactor part (on the curve, not in
+G2: pairing's into_affine rejects it), an absent share, and one instance left with
+fewer than t shares (NotEnoughShares).  coin_n128 is BASELINE config 4's shape (N = 128, t = 43)
+for 4 instances (sessions 0/1, proposers 0, 1, 127) with 1 in 64 shares signed over another
+nonce.  Expected: HBX_SHARE_* status per share (common_coin.rs:151), combined signature of the
+first t valid shares in index order (:190), master verification (:196), parity (:173).
 """
 from __future__ import annotations
 
+import multiprocessing as mp
 import os
 import sys
 
@@ -25,14 +29,36 @@ from oracle import threshold as tc  # noqa: E402
 from oracle.chacha_rand04 import ChaChaRng04  # noqa: E402
 
 
-def make(n: int):
+SHARE_INVALID, SHARE_VALID, SHARE_ABSENT, SHARE_UNDECODABLE = 0, 1, 2, 3
+
+
+def cofactor_point():
+    """A nonzero point of E'(Fq2) killed by... nothing in G2: r * P for a random curve point P."""
+    x0 = 5
+    while True:
+        x = (x0, 3)
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is not None:
+            t = bls.g2_mul((x, y), bls.R)
+            if t is not None:
+                return t
+        x0 += 1
+
+
+def _verify(args):
+    pk, sig, h = args
+    return bls.pairing_product_is_one([(pk, h), (bls.g1_neg(bls.G1_GEN), sig)])
+
+
+def make(n: int, pool=None):
     f = (n - 1) // 3
     t = f + 1
     rng = ChaChaRng04([0x68626278, 0x10 + n])
     sks = tc.SecretKeySet.random(f, rng)
     pks = sks.public_keys()
     inv_id = tc.PublicKeySet.to_bytes(pks)
-    specs = [(0, 0), (0, 1), (1, 2)]                    # (session, proposer)
+    big = n > 16
+    specs = [(0, 0), (0, 1), (1, 0), (1, n - 1)] if big else [(0, 0), (0, 1), (1, 2)]  # (session, proposer)
     nonces = [tc.nonce_bytes(inv_id, s, p, 2) for s, p in specs]
     hs = [tc.hash_g2(x) for x in nonces]
     count = len(nonces)
@@ -43,26 +69,47 @@ def make(n: int):
         for i in range(n):
             pts[(c, i)] = tc.sign(sks.secret_key_share(i), nonces[c], hash_pt=hs[c])
     other = tc.hash_g2(b"some other nonce")
-    pts[(0, n - 1)] = tc.sign(sks.secret_key_share(n - 1), b"", hash_pt=other)   # wrong message
+    wrong = [(0, n - 1)]
+    if big:
+        crng = np.random.default_rng([0x68626278, 0x20 + n])
+        wrong = [(c, i) for c in range(count) for i in range(n) if crng.integers(0, 64) == 0]
+    for (c, i) in wrong:
+        pts[(c, i)] = tc.sign(sks.secret_key_share(i), b"", hash_pt=other)   # a signature of another message
     for (c, i), p in pts.items():
         sigs[c, i] = np.frombuffer(bls.g2_compress(p), dtype=np.uint8)
-    sigs[1, 0] = 0xFF                                   # undecodable (x >= p)
-    sigs[1, 0, 0] = 0x9F
-    present[1, min(2, n - 1)] = False
-    present[2, 1:] = False                              # starve instance 2: 1 share < t
-    expect_valid = np.zeros((count, n), dtype=bool)
+    undecodable = set()
+    if not big:
+        sigs[1, 0] = 0xFF                               # undecodable (x >= p)
+        sigs[1, 0, 0] = 0x9F
+        torsion = bls.g2_add(pts[(0, 1)], cofactor_point())
+        sigs[0, 1] = np.frombuffer(bls.g2_compress(torsion), dtype=np.uint8)  # honest + cofactor part
+        undecodable = {(1, 0), (0, 1)}
+        present[1, min(2, n - 1)] = False
+        present[2, 1:] = False                          # starve instance 2: 1 share < t
+    status = np.full((count, n), SHARE_ABSENT, dtype=np.uint8)
+    jobs, where = [], []
     for c in range(count):
         for i in range(n):
-            if present[c, i] and (c, i) != (1, 0):
-                expect_valid[c, i] = tc.verify_sig(pks.public_key_share(i), pts[(c, i)], nonces[c], hash_pt=hs[c])
-    status = np.zeros(count, dtype=np.int32)
+            if not present[c, i]:
+                continue
+            if (c, i) in undecodable:
+                status[c, i] = SHARE_UNDECODABLE
+                continue
+            jobs.append((pks.public_key_share(i), pts[(c, i)], hs[c]))
+            where.append((c, i))
+    res = pool.map(_verify, jobs, chunksize=8) if pool is not None else list(map(_verify, jobs))
+    for (c, i), ok in zip(where, res):
+        status[c, i] = SHARE_VALID if ok else SHARE_INVALID
+        assert ok == ((c, i) not in wrong)
+    expect_valid = status == SHARE_VALID
+    comb_status = np.zeros(count, dtype=np.int32)
     sig_out = np.zeros((count, 96), dtype=np.uint8)
     master_ok = np.zeros(count, dtype=bool)
     parity = np.zeros(count, dtype=bool)
     for c in range(count):
         shares = [(i, pts[(c, i)]) for i in range(n) if expect_valid[c, i]]
         if len(shares) < t:
-            status[c] = -3
+            comb_status[c] = -3
             continue
         sig = tc.combine_signatures(pks, shares)
         sig_out[c] = np.frombuffer(bls.g2_compress(sig), dtype=np.uint8)
@@ -77,14 +124,17 @@ def make(n: int):
         sk=np.stack([np.frombuffer(sks.secret_key_share(i).to_bytes(32, "big"), dtype=np.uint8) for i in range(n)]),
         nonce_blob=np.frombuffer(b"".join(nonces), dtype=np.uint8), nonce_off=off,
         h=np.stack([np.frombuffer(bls.g2_compress(h), dtype=np.uint8) for h in hs]),
-        sigs=sigs, present=present, expect_valid=expect_valid, expect_status=status, expect_sig=sig_out,
+        sigs=sigs, present=present, expect_valid=expect_valid, expect_share_status=status,
+        expect_status=comb_status, expect_sig=sig_out,
         expect_master_ok=master_ok, expect_parity=parity,
     )
 
 
 def main():
-    for n in (4, 7):
-        d = make(n)
+    ns = [int(x) for x in sys.argv[1:]] or [4, 7, 128]
+    pool = mp.Pool(min(8, os.cpu_count() or 1))
+    for n in ns:
+        d = make(n, pool)
         path = os.path.join(HERE, f"coin_n{n}.npz")
         np.savez_compressed(path, **d)
         print(path, "valid", int(d["expect_valid"].sum()), "status", d["expect_status"].tolist(),

@@ -26,7 +26,8 @@ def test_port_matches_fixture(port, n):
     d = dict(np.load(os.path.join(ROOT, "tests", "golden", f"hb_epoch_n{n}.npz"), allow_pickle=False))
     p = len(d["v_off"]) - 1
     nn = d["shares"].shape[1]
-    jobs = [(j, i) for j in range(p) for i in range(nn) if d["present"][j, i] and d["expect_ct_valid"][j]]
+    # shares that reach a verification (not absent, decodable, ciphertext valid)
+    jobs = [(j, i) for j in range(p) for i in range(nn) if d["expect_share_status"][j, i] in (0, 1)]
     assert jobs
     J = np.array(jobs, dtype=np.uint32)
     out = np.zeros(len(jobs), dtype=np.uint8)

@@ -16,14 +16,30 @@ def _load(n):
     return dict(np.load(os.path.join(GOLDEN, f"hb_epoch_n{n}.npz"), allow_pickle=False))
 
 
-@pytest.mark.parametrize("n", [4, 7])
+@pytest.mark.parametrize("n", [4, 7, 10])
 def test_fixture_shape(n):
     d = _load(n)
     p = len(d["v_off"]) - 1
     assert d["shares"].shape == (p, n, 48) and d["expect_valid"].shape == (p, n)
     assert int(d["t"]) == (n - 1) // 3 + 1
-    assert not d["expect_ct_valid"][0] and d["expect_ct_valid"][1:].all()
-    assert d["expect_status"][0] == -7 and d["expect_status"][-1] == -3
+    assert str(d["digest"]) == "sha256"
+    # edge cases present: ShareDecryptionFailed, a valid ct, every share status but UNKNOWN_SENDER
+    assert d["expect_ct_status"][0] == 0 and (d["expect_ct_status"] == 1).any()
+    assert set(np.unique(d["expect_share_status"]).tolist()) == {0, 1, 2, 3, 4}
+    assert d["expect_status"][0] == -7
+    assert (d["expect_valid"] == (d["expect_share_status"] == 1)).all()
+
+
+@pytest.mark.parametrize("name", ["hb_epoch_n64", "hb_cols_n256"])
+def test_big_fixture_shape(name):
+    d = dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+    n = int(d["n"])
+    p = len(d["v_off"]) - 1
+    assert d["shares"].shape == (p, n, 48)
+    assert (d["expect_ct_status"] == 1).all() and (d["expect_status"] == 0).all()
+    # validity == not corrupted (FaultyShareAdversary positions), verified by the oracle at generation
+    assert ((d["expect_share_status"] == 1) == ~d["corrupt"]).all()
+    assert d["corrupt"].any()
 
 
 @pytest.mark.parametrize("n", [4])
@@ -39,18 +55,27 @@ def test_fixture_against_oracle(n):
         h = tc.hash_g1_g2(u, v)
         assert bls.g2_compress(h) == d["h"][j].tobytes()
         assert tc.ciphertext_verify((u, v, w), hash_pt=h) == bool(d["expect_ct_valid"][j])
-    # sample: proposer 1 (valid ct, one corrupted + one absent share)
-    j = 1
-    u = bls.g1_decompress(d["u"][j].tobytes())
-    v = d["v_blob"][int(off[j]):int(off[j + 1])].tobytes()
-    w = bls.g2_decompress(d["w"][j].tobytes())
-    h = bls.g2_decompress(d["h"][j].tobytes())
-    for i in range(n):
-        if not d["present"][j, i]:
-            assert not d["expect_valid"][j, i]
+    # every share of every valid proposer: status == the oracle's decode + verification
+    for j in range(p):
+        if d["expect_ct_status"][j] != 1:
+            assert set(d["expect_share_status"][j][d["present"][j]].tolist()) <= {4}
             continue
-        s = bls.g1_decompress(d["shares"][j, i].tobytes())
-        assert tc.verify_decryption_share(pks[i], s, (u, v, w), hash_pt=h) == bool(d["expect_valid"][j, i])
+        u = bls.g1_decompress(d["u"][j].tobytes())
+        v = d["v_blob"][int(off[j]):int(off[j + 1])].tobytes()
+        w = bls.g2_decompress(d["w"][j].tobytes())
+        h = bls.g2_decompress(d["h"][j].tobytes())
+        for i in range(n):
+            st = int(d["expect_share_status"][j, i])
+            if not d["present"][j, i]:
+                assert st == 2
+                continue
+            try:
+                s = bls.g1_decompress(d["shares"][j, i].tobytes())
+            except ValueError:
+                assert st == 3
+                continue
+            ok = tc.verify_decryption_share(pks[i], s, (u, v, w), hash_pt=h)
+            assert st == (1 if ok else 0), (j, i)
 
 
 @pytest.mark.parametrize("n", [4])

@@ -1,7 +1,8 @@
 """GPU parity for the Common Coin path against the committed oracle
-fixtures tests/golden/coin_n{4,7}.npz (tests/golden/make_coin_golden.py): hash_g2 of the nonces,
-signature-share validity, combined signature, master verification, parity, and the producer-side
-SecretKeyShare::sign.  Bit-exact."""
+fixtures tests/golden/coin_n{4,7,128}.npz (tests/golden/make_coin_golden.py; N = 128 is BASELINE
+config 4's shape): hash_g2 of the nonces, HBX_SHARE_* status of every signature share (including
+an honest share plus a cofactor-part point, which must be rejected as off-subgroup), combined
+signature, master verification, parity, and the producer-side SecretKeyShare::sign.  Bit-exact."""
 import os
 
 import numpy as np
@@ -20,7 +21,7 @@ def _nonces(d):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7])
+@pytest.mark.parametrize("n", [4, 7, 128])
 def test_coin_matches_golden(hbx_ctx, n):
     d = _load(n)
     assert (hbx_ctx.set_pk_shares([r.tobytes() for r in d["pk_comp"]]) == 0).all()
@@ -28,6 +29,8 @@ def test_coin_matches_golden(hbx_ctx, n):
     np.testing.assert_array_equal(h, d["h"])
     valid = hbx_ctx.verify_sig_shares(d["sigs"], d["present"])
     np.testing.assert_array_equal(valid, d["expect_valid"])
+    count, nn = d["sigs"].shape[:2]
+    np.testing.assert_array_equal(hbx_ctx.sig_share_status(count, nn), d["expect_share_status"])
     sig, st, ok, par = hbx_ctx.combine_signatures(d["master_pk"].tobytes(), int(d["t"]))
     np.testing.assert_array_equal(st, d["expect_status"])
     good = st == 0
@@ -38,8 +41,9 @@ def test_coin_matches_golden(hbx_ctx, n):
 
 
 @pytest.mark.gpu
-def test_sign_matches_honest_shares(hbx_ctx):
-    d = _load(4)
+@pytest.mark.parametrize("n", [4, 128])
+def test_sign_matches_honest_shares(hbx_ctx, n):
+    d = _load(n)
     hbx_ctx.prepare_nonces(_nonces(d))
     sigs = hbx_ctx.sign(d["sk"])
     honest = d["expect_valid"]

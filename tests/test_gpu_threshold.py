@@ -1,15 +1,21 @@
-"""GPU parity: threshold decryption path vs the committed oracle fixtures (SURVEY.md §8 rows
-A1, A2, A4, A5).  Bit-exact: validity bits, ciphertext bits, per-proposer status, plaintext bytes."""
+"""GPU parity: threshold decryption path vs the committed oracle fixtures (SURVEY.md §8 rows A1,
+A2, A4-A8, f1, f2) at every BASELINE config (tests/golden/make_golden.py): N = 4, 7 (every edge
+case), N = 10 (config 1), N = 64 (config 2, a full epoch), N = 256 (config 3, four proposer
+columns incl. a 1 MiB ciphertext).  Bit-exact: HBX_CT_* / HBX_SHARE_* statuses, validity bits,
+hoisted H_j bytes, per-proposer combine status and plaintext bytes, in the three-call host API,
+the fused device call and own-share mode; producer side (public keys, encrypt, decryption shares)."""
+import hashlib
 import os
 
 import numpy as np
 import pytest
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+FIXTURES = ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256"]
 
 
-def _load(n):
-    return dict(np.load(os.path.join(GOLDEN, f"hb_epoch_n{n}.npz"), allow_pickle=False))
+def _load(name):
+    return dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
 
 
 def _cts(d):
@@ -18,103 +24,186 @@ def _cts(d):
             for j in range(len(off) - 1)]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7])
-def test_epoch_matches_golden(hbx_ctx, n):
-    d = _load(n)
-    st = hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]])
+def _check_plain(d, j, pt: bytes, own=False):
+    key = "expect_plain_sha_own" if own else "expect_plain_sha"
+    assert hashlib.sha256(pt).digest() == d[key][j].tobytes(), f"plaintext {j}"
+
+
+def _set_keys(ctx, d):
+    st = ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]])
     assert (st == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+def test_epoch_matches_golden(hbx_ctx, name):
+    d = _load(name)
+    assert str(d["digest"]) == "sha256"
+    _set_keys(hbx_ctx, d)
+    p, n = d["shares"].shape[:2]
     ct_ok = hbx_ctx.prepare_ciphertexts(_cts(d))
     np.testing.assert_array_equal(ct_ok, d["expect_ct_valid"])
+    np.testing.assert_array_equal(hbx_ctx.ct_status(p), d["expect_ct_status"])
+    # H_j = hash_g1_g2(U_j, V_j) bytes for every ciphertext that decodes
+    h = hbx_ctx.ct_hashes(p)
+    dec = d["expect_ct_status"] != 3
+    np.testing.assert_array_equal(h[dec], d["h"][dec])
     valid = hbx_ctx.verify_dec_shares(d["shares"], d["present"])
     np.testing.assert_array_equal(valid, d["expect_valid"])
+    np.testing.assert_array_equal(hbx_ctx.share_status(p, n), d["expect_share_status"])
     plains, status = hbx_ctx.combine_decrypt(int(d["t"]))
     np.testing.assert_array_equal(status, d["expect_status"])
-    off = d["v_off"]
     for j, pt in enumerate(plains):
         if status[j] == 0:
-            assert pt == d["expect_plain_blob"][int(off[j]):int(off[j + 1])].tobytes()
+            _check_plain(d, j, pt)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7])
-def test_fused_epoch_call_matches_golden(hbx_ctx, n):
-    """hbx_decrypt_epoch_d (Ciphertext::verify on the second stream beside the speculative
-    combine) gives the fixture's bits, statuses and plaintexts, invalid ciphertext included."""
+def _device_epoch(ctx, d, own: bool):
     import torch
 
-    d = _load(n)
-    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
     dev = torch.device("cuda", 0)
-    p = len(d["v_off"]) - 1
-    nn = d["shares"].shape[1]
+    p, n = d["shares"].shape[:2]
     off = d["v_off"].astype(np.int64)
     t_u = torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev)
     t_w = torch.from_numpy(np.ascontiguousarray(d["w"])).to(dev)
-    t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"]).astype(np.uint8).copy() if len(d["v_blob"]) else np.zeros(1, np.uint8)).to(dev)
+    t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"]).copy() if len(d["v_blob"]) else np.zeros(1, np.uint8)).to(dev)
     t_off = torch.from_numpy(off).to(dev)
     t_sh = torch.from_numpy(np.ascontiguousarray(d["shares"])).to(dev)
     t_pr = torch.from_numpy(np.ascontiguousarray(d["present"]).astype(np.uint8)).to(dev)
     t_out = torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
-    t_valid = torch.zeros(p * nn, dtype=torch.uint8, device=dev)
+    t_valid = torch.zeros(p * n, dtype=torch.uint8, device=dev)
     t_ct = torch.zeros(p, dtype=torch.uint8, device=dev)
     t_st = torch.zeros(p, dtype=torch.int32, device=dev)
     maxv = int(np.max(np.diff(off))) if p else 0
-    hbx_ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, p, maxv, t_sh, nn, int(d["t"]), t_out, d_valid=t_valid,
-                            d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(t_ct.cpu().numpy(), d["expect_ct_valid"])
-    np.testing.assert_array_equal(t_valid.cpu().numpy().reshape(p, nn), d["expect_valid"].reshape(p, nn))
+    # default stream: the tensors above were uploaded on torch's current stream, and the binding
+    # enqueues on that same stream (no extra synchronisation needed)
+    ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, p, maxv, t_sh, n, int(d["t"]), t_out, d_valid=t_valid,
+                        d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
+    sfx = "_own" if own else ""
+    np.testing.assert_array_equal(t_ct.cpu().numpy(), d["expect_ct_status"])
+    np.testing.assert_array_equal(t_valid.cpu().numpy().reshape(p, n), d["expect_share_status" + sfx])
     status = t_st.cpu().numpy()
-    np.testing.assert_array_equal(status, d["expect_status"])
+    np.testing.assert_array_equal(status, d["expect_status" + sfx])
     out = t_out.cpu().numpy()
     for j in range(p):
         if status[j] == 0:
-            assert out[off[j]:off[j + 1]].tobytes() == d["expect_plain_blob"][int(off[j]):int(off[j + 1])].tobytes()
+            _check_plain(d, j, out[off[j]:off[j + 1]].tobytes(), own)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7])
-def test_own_share_mode_matches_golden(hbx_ctx, n):
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fused_epoch_call_matches_golden(hbx_ctx, name):
+    """hbx_decrypt_epoch_d: statuses, combine statuses and plaintexts of the fixture in one call
+    (Ciphertext::verify deferred into the share-check launch)."""
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
+    _device_epoch(hbx_ctx, d, own=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+def test_own_share_mode_matches_golden(hbx_ctx, name):
     """hbx_set_own_share: node `me`'s own share replaces its input row, and that share's check is
-    Ciphertext::verify (no separate ciphertext checks).  The fixture's own-mode expectations come
-    from the oracle (tests/golden/make_golden.py): the invalid ciphertext is still caught, and the
-    starved proposer gains our honest share."""
-    d = _load(n)
-    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
+    Ciphertext::verify.  Host API (immediate ct checks) and the fused device call."""
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
     me = int(d["own_me"])
+    p, n = d["shares"].shape[:2]
     hbx_ctx.set_own_share(me, d["own_sk"].tobytes())
     try:
-        ct_ok = hbx_ctx.prepare_ciphertexts(_cts(d))  # immediate Ciphertext::verify (wide path)
+        ct_ok = hbx_ctx.prepare_ciphertexts(_cts(d))
         np.testing.assert_array_equal(ct_ok, d["expect_ct_valid"])
         valid = hbx_ctx.verify_dec_shares(d["shares"], d["present"])
         np.testing.assert_array_equal(valid, d["expect_valid_own"])
+        np.testing.assert_array_equal(hbx_ctx.share_status(p, n), d["expect_share_status_own"])
         plains, status = hbx_ctx.combine_decrypt(int(d["t"]))
         np.testing.assert_array_equal(status, d["expect_status_own"])
-        off = d["v_off"]
         for j, pt in enumerate(plains):
             if status[j] == 0:
-                assert pt == d["expect_plain_blob_own"][int(off[j]):int(off[j + 1])].tobytes()
-        # deferred ciphertext checks: the own share's lane decides ct validity
-        import torch
-
-        dev = torch.device("cuda", 0)
-        p = len(off) - 1
-        t_u = torch.from_numpy(np.ascontiguousarray(d["u"])).to(dev)
-        t_w = torch.from_numpy(np.ascontiguousarray(d["w"])).to(dev)
-        t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"]).copy()).to(dev)
-        t_off = torch.from_numpy(off.astype(np.int64)).to(dev)
-        t_sh = torch.from_numpy(np.ascontiguousarray(d["shares"])).to(dev)
-        t_pr = torch.from_numpy(np.ascontiguousarray(d["present"]).astype(np.uint8)).to(dev)
-        t_out = torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
-        t_valid = torch.zeros(p * n, dtype=torch.uint8, device=dev)
-        t_ct = torch.zeros(p, dtype=torch.uint8, device=dev)
-        t_st = torch.zeros(p, dtype=torch.int32, device=dev)
-        hbx_ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, p, int(np.max(np.diff(off))), t_sh, n, int(d["t"]), t_out,
-                                d_valid=t_valid, d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(t_ct.cpu().numpy(), d["expect_ct_valid"])
-        np.testing.assert_array_equal(t_valid.cpu().numpy().reshape(p, n), d["expect_valid_own"])
-        np.testing.assert_array_equal(t_st.cpu().numpy(), d["expect_status_own"])
+                _check_plain(d, j, pt, own=True)
+        _device_epoch(hbx_ctx, d, own=True)
     finally:
         hbx_ctx.set_own_share(me, None)
+
+
+@pytest.mark.gpu
+def test_unknown_sender_status(hbx_ctx):
+    """Senders >= n of hbx_set_pk_shares: HBX_SHARE_UNKNOWN_SENDER (the reference returns
+    Err(UnknownSender), honey_badger.rs:64-66), never a verification."""
+    d = _load("hb_epoch_n7")
+    n = d["shares"].shape[1]
+    hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"][: n - 2]])
+    p = d["shares"].shape[0]
+    hbx_ctx.prepare_ciphertexts(_cts(d))
+    hbx_ctx.verify_dec_shares(d["shares"], d["present"])
+    st = hbx_ctx.share_status(p, n)
+    want = d["expect_share_status"].copy()
+    want[:, n - 2:] = np.where(d["present"][:, n - 2:], 5, 2)
+    np.testing.assert_array_equal(st, want)
+
+
+@pytest.mark.gpu
+def test_combine_needs_verify_after_prepare(hbx_ctx):
+    """A prepare invalidates the previous verification: combine before the next verify is an
+    error (HBX_E_NO_CIPHERTEXTS), not a decryption with the old shares."""
+    from hbbft_amd.hbx import HBX_E_NO_CIPHERTEXTS, HbxError
+
+    d = _load("hb_epoch_n4")
+    _set_keys(hbx_ctx, d)
+    hbx_ctx.prepare_ciphertexts(_cts(d))
+    hbx_ctx.verify_dec_shares(d["shares"], d["present"])
+    hbx_ctx.prepare_ciphertexts(_cts(d))
+    with pytest.raises(HbxError) as e:
+        hbx_ctx.combine_decrypt(int(d["t"]))
+    assert e.value.code == HBX_E_NO_CIPHERTEXTS
+
+
+@pytest.mark.gpu
+def test_key_change_clears_own_share(hbx_ctx):
+    """hbx_set_pk_shares starts a new era: the own share of the old keys is dropped, so the next
+    epoch runs in plain mode instead of checking ciphertexts with a stale secret."""
+    d = _load("hb_epoch_n7")
+    _set_keys(hbx_ctx, d)
+    hbx_ctx.set_own_share(int(d["own_me"]), d["own_sk"].tobytes())
+    _set_keys(hbx_ctx, d)  # new era (same keys here): own share cleared
+    _device_epoch(hbx_ctx, d, own=False)
+
+
+# ---- producer side (SURVEY.md §8(a) A6, §8(f) item 2) ------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n64", "hb_cols_n256"])
+def test_public_keys_match_oracle(hbx_ctx, name):
+    d = _load(name)
+    np.testing.assert_array_equal(hbx_ctx.public_keys(d["sk_shares"]), d["pk_comp"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n10", "hb_cols_n256"])
+def test_encrypt_matches_oracle(hbx_ctx, name):
+    """PublicKey::encrypt with given r_j: U, V, W bytes equal the oracle's (honey_badger.rs:116)."""
+    d = _load(name)
+    off = d["enc_msg_off"]
+    p = len(off) - 1
+    msgs = [d["enc_msg_blob"][int(off[j]):int(off[j + 1])].tobytes() for j in range(p)]
+    cts = hbx_ctx.encrypt(d["master_pk"].tobytes(), msgs, d["enc_r"])
+    voff = d["v_off"]
+    for j in range(p):
+        if not d["enc_ok"][j]:
+            continue
+        u, v, w = cts[j]
+        assert u == d["enc_u"][j].tobytes(), f"U {j}"
+        assert w == d["enc_w"][j].tobytes(), f"W {j}"
+        assert v == d["v_blob"][int(voff[j]):int(voff[j + 1])].tobytes(), f"V {j}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n64", "hb_cols_n256"])
+def test_decrypt_shares_match_oracle(hbx_ctx, name):
+    """decrypt_share_no_verify: S_ji = sk_i U_j bytes equal the fixture's honest shares."""
+    d = _load(name)
+    keep = d["enc_ok"] & (d["expect_ct_status"] != 3)
+    u = d["enc_u"][keep]
+    sh = hbx_ctx.decrypt_shares(d["sk_shares"], u)
+    want = d["shares"][keep]
+    mask = ~d["corrupt"][keep] & d["present"][keep] & (d["expect_share_status"][keep] != 3)
+    np.testing.assert_array_equal(sh[mask], want[mask])

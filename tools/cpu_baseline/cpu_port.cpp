@@ -36,6 +36,7 @@ g2j g2_rand_reference_shape(chacha_rng& r) {
   }
 }
 fq12 pairing(const g1a& P, const g2a& Q) {
+  if (P.inf || Q.inf) return fq12_one();  // e(O, Q) = e(P, O) = 1
   line_pre L[MILLER_LINES];
   fq2 scratch[2 * MILLER_LINES];
   g2_prepare_lines(Q, L, scratch);
@@ -63,9 +64,11 @@ int cpu_verify_dec_shares(const uint8_t* pk48, uint32_t n, const uint8_t* u48, c
       const uint32_t j = jobs[2 * k], i = jobs[2 * k + 1];
       g1a pk, S, U;
       g2a W;
-      if (g1_decompress(pk48 + (size_t)i * 48, pk) != HBX_PT_OK || g1_decompress(u48 + (size_t)j * 48, U) != HBX_PT_OK ||
-          g2_decompress(w96 + (size_t)j * 96, W) != HBX_PT_OK ||
-          g1_decompress(shares48 + ((size_t)j * n + i) * 48, S) != HBX_PT_OK) {
+      // deserialisation (the identity decodes; HBX_PT_INFINITY sets .inf)
+      auto ok1 = [](int st) { return st == HBX_PT_OK || st == HBX_PT_INFINITY; };
+      if (!ok1(g1_decompress(pk48 + (size_t)i * 48, pk)) || !ok1(g1_decompress(u48 + (size_t)j * 48, U)) ||
+          !ok1(g2_decompress(w96 + (size_t)j * 96, W)) ||
+          !ok1(g1_decompress(shares48 + ((size_t)j * n + i) * 48, S))) {
         out[k] = 0;
         continue;
       }

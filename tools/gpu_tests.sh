@@ -1,3 +1,2 @@
-set -e
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_r2b.txt 2>&1
+echo "pytest rc=$?" >> gpurun_out/pytest_gpu_r2b.txt
