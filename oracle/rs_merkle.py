@@ -174,26 +174,36 @@ class ReedSolomon:
 # ---------------------------------------------------------------------------------------------
 # Merkle tree (merkle.rs with ring SHA-256)
 # ---------------------------------------------------------------------------------------------
-def hash_leaf(value: bytes) -> bytes:
+# Two tree digests (include/hbx.h HBX_MERKLE_*):
+#   "sha256": merkle (afck fork) + ring SHA-256 -- leaf H(0x00 || v), node H(0x01 || l || r);
+#   "sha3":   later hbbft's own src/broadcast/merkle.rs (tiny-keccak) -- leaf SHA3-256(v), node
+#             SHA3-256(l || r); same level structure (pairs left to right, odd node promoted).
+#             Restated from the published later hbbft source as remembered: parity unpinned.
+def hash_leaf(value: bytes, variant: str = "sha256") -> bytes:
+    if variant == "sha3":
+        return hashlib.sha3_256(bytes(value)).digest()
     return hashlib.sha256(b"\x00" + bytes(value)).digest()
 
 
-def hash_nodes(left: bytes, right: bytes) -> bytes:
+def hash_nodes(left: bytes, right: bytes, variant: str = "sha256") -> bytes:
+    if variant == "sha3":
+        return hashlib.sha3_256(left + right).digest()
     return hashlib.sha256(b"\x01" + left + right).digest()
 
 
 class MerkleTree:
     """MerkleTree::from_vec: levels paired left to right, odd trailing node promoted."""
 
-    def __init__(self, values):
+    def __init__(self, values, variant: str = "sha256"):
+        self.variant = variant
         self.values = [bytes(v) for v in values]
         if not self.values:
             self.levels = [[hashlib.sha256(b"").digest()]]
             return
-        level = [hash_leaf(v) for v in self.values]
+        level = [hash_leaf(v, variant) for v in self.values]
         self.levels = [level]
         while len(level) > 1:
-            nxt = [hash_nodes(level[i], level[i + 1]) for i in range(0, len(level) - 1, 2)]
+            nxt = [hash_nodes(level[i], level[i + 1], variant) for i in range(0, len(level) - 1, 2)]
             if len(level) % 2:
                 nxt.append(level[-1])
             self.levels.append(nxt)
@@ -229,18 +239,18 @@ class MerkleTree:
         return {"root_hash": self.root_hash(), "lemma": lemma, "value": bytes(value)}
 
 
-def proof_validate(proof, root_hash: bytes) -> bool:
+def proof_validate(proof, root_hash: bytes, variant: str = "sha256") -> bool:
     """merkle.rs Proof::validate."""
     lemma = proof["lemma"]
     if proof["root_hash"] != root_hash or lemma[0][0] != root_hash:
         return False
     for k, (node_hash, sib) in enumerate(lemma):
         if k == len(lemma) - 1:
-            return sib is None and hash_leaf(proof["value"]) == node_hash
+            return sib is None and hash_leaf(proof["value"], variant) == node_hash
         if sib is None:
             return False
         sub_hash = lemma[k + 1][0]
-        combined = hash_nodes(sib[1], sub_hash) if sib[0] == "L" else hash_nodes(sub_hash, sib[1])
+        combined = hash_nodes(sib[1], sub_hash, variant) if sib[0] == "L" else hash_nodes(sub_hash, sib[1], variant)
         if combined != node_hash:
             return False
     return False
@@ -261,9 +271,9 @@ def proof_index(proof, count: int) -> int:
     return idx
 
 
-def validate_broadcast_proof(proof, node_index: int, n: int) -> bool:
+def validate_broadcast_proof(proof, node_index: int, n: int, variant: str = "sha256") -> bool:
     """Broadcast::validate_proof (broadcast.rs:555-575)."""
-    return (proof_validate(proof, proof["root_hash"]) and len(proof["value"]) > 0
+    return (proof_validate(proof, proof["root_hash"], variant) and len(proof["value"]) > 0
             and node_index == proof["value"][0] and proof_index(proof, n) == proof["value"][0])
 
 
@@ -291,14 +301,14 @@ def frame_shards(value: bytes, n: int) -> np.ndarray:
     return buf
 
 
-def send_shards(value: bytes, n: int):
+def send_shards(value: bytes, n: int, variant: str = "sha256"):
     """Frame, RS-encode, index-prefix: returns (shards uint8[n, L], leaves, tree)."""
     k, m = coding_counts(n)
     buf = frame_shards(value, n)
     if m > 0:
         buf = ReedSolomon(k, m).encode(buf)
     leaves = [bytes([i & 0xFF]) + buf[i].tobytes() for i in range(n)]
-    return buf, leaves, MerkleTree(leaves)
+    return buf, leaves, MerkleTree(leaves, variant)
 
 
 def glue_shards(leaves, k: int):
@@ -309,7 +319,7 @@ def glue_shards(leaves, k: int):
     return data[4:4 + ln]
 
 
-def decode_from_shards(leaf_values, n: int, root_hash: bytes):
+def decode_from_shards(leaf_values, n: int, root_hash: bytes, variant: str = "sha256"):
     """broadcast.rs:660-692: reconstruct (index byte included), rebuild the tree, compare the root,
     glue.  leaf_values: list of n (bytes or None).  Returns the value or None."""
     k, m = coding_counts(n)
@@ -322,6 +332,6 @@ def decode_from_shards(leaf_values, n: int, root_hash: bytes):
         if any(v is None for v in leaf_values):
             return None
         leaves = [bytes(v) for v in leaf_values]
-    if MerkleTree(leaves).root_hash() != root_hash:
+    if MerkleTree(leaves, variant).root_hash() != root_hash:
         return None
     return glue_shards(leaves, k)

@@ -20,3 +20,13 @@ def hbx_ctx():
     ctx = Context(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(autouse=True)
+def _default_digests(request):
+    """Every GPU test starts with the default digests (SHA-256 threshold hashing, afck Merkle)."""
+    if "hbx_ctx" in request.fixturenames:
+        ctx = request.getfixturevalue("hbx_ctx")
+        ctx.set_digest(0)
+        ctx.set_merkle_digest(0)
+    yield

@@ -50,7 +50,7 @@ def _verify(args):
     return bls.pairing_product_is_one([(pk, h), (bls.g1_neg(bls.G1_GEN), sig)])
 
 
-def make(n: int, pool=None):
+def make(n: int, pool=None, digest: str = "sha256"):
     f = (n - 1) // 3
     t = f + 1
     rng = ChaChaRng04([0x68626278, 0x10 + n])
@@ -60,7 +60,7 @@ def make(n: int, pool=None):
     big = n > 16
     specs = [(0, 0), (0, 1), (1, 0), (1, n - 1)] if big else [(0, 0), (0, 1), (1, 2)]  # (session, proposer)
     nonces = [tc.nonce_bytes(inv_id, s, p, 2) for s, p in specs]
-    hs = [tc.hash_g2(x) for x in nonces]
+    hs = [tc.hash_g2(x, digest) for x in nonces]
     count = len(nonces)
     sigs = np.zeros((count, n, 96), dtype=np.uint8)
     present = np.ones((count, n), dtype=bool)
@@ -68,7 +68,7 @@ def make(n: int, pool=None):
     for c in range(count):
         for i in range(n):
             pts[(c, i)] = tc.sign(sks.secret_key_share(i), nonces[c], hash_pt=hs[c])
-    other = tc.hash_g2(b"some other nonce")
+    other = tc.hash_g2(b"some other nonce", digest)
     wrong = [(0, n - 1)]
     if big:
         crng = np.random.default_rng([0x68626278, 0x20 + n])
@@ -118,7 +118,7 @@ def make(n: int, pool=None):
     off = np.zeros(count + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(x) for x in nonces])
     return dict(
-        n=np.int64(n), t=np.int64(t),
+        digest=np.array(digest), n=np.int64(n), t=np.int64(t),
         pk_comp=np.stack([np.frombuffer(bls.g1_compress(pks.public_key_share(i)), dtype=np.uint8) for i in range(n)]),
         master_pk=np.frombuffer(bls.g1_compress(pks.public_key()), dtype=np.uint8),
         sk=np.stack([np.frombuffer(sks.secret_key_share(i).to_bytes(32, "big"), dtype=np.uint8) for i in range(n)]),
@@ -131,11 +131,13 @@ def make(n: int, pool=None):
 
 
 def main():
-    ns = [int(x) for x in sys.argv[1:]] or [4, 7, 128]
+    specs = [(a.split("_")[0], "_".join(a.split("_")[1:]) or "sha256") for a in sys.argv[1:]] or \
+        [("4", "sha256"), ("7", "sha256"), ("128", "sha256"), ("4", "sha3_256")]
     pool = mp.Pool(min(8, os.cpu_count() or 1))
-    for n in ns:
-        d = make(n, pool)
-        path = os.path.join(HERE, f"coin_n{n}.npz")
+    for ns, dg in specs:
+        n = int(ns)
+        d = make(n, pool, dg)
+        path = os.path.join(HERE, f"coin_n{n}" + ("" if dg == "sha256" else "_sha3") + ".npz")
         np.savez_compressed(path, **d)
         print(path, "valid", int(d["expect_valid"].sum()), "status", d["expect_status"].tolist(),
               "master_ok", d["expect_master_ok"].tolist(), "parity", d["expect_parity"].astype(int).tolist())

@@ -58,6 +58,8 @@ FIXTURES = {
     "hb_epoch_n10": (10, 10, [100, 1024, 7, 65, 300], True, 0),
     "hb_epoch_n64": (64, 64, [1024], False, 64),
     "hb_cols_n256": (256, 4, [1 << 20, 1024, 64, 1], False, 64),
+    # DIGEST = SHA3-256 (tiny-keccak threshold_crypto revisions; hbx_set_digest)
+    "hb_epoch_n7_sha3": (7, 7, [1, 64, 65, 200], True, 0, "sha3_256"),
 }
 
 
@@ -91,7 +93,7 @@ def _sha(b: bytes) -> np.ndarray:
     return np.frombuffer(hashlib.sha256(b).digest(), dtype=np.uint8)
 
 
-def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool):
+def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool, digest: str = "sha256"):
     f = (n - 1) // 3
     t = f + 1
     sks = tc.SecretKeySet.random(f, ChaChaRng04([SEED, 1]))
@@ -105,10 +107,10 @@ def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool):
         ln = v_lens[j % len(v_lens)]
         msg = data_rng.integers(0, 256, size=ln, dtype=np.uint8).tobytes()
         r = tc.fr_rand(r_rng)
-        honest.append(tc.encrypt(pks.public_key(), msg, r))
+        honest.append(tc.encrypt(pks.public_key(), msg, r, digest))
         msgs.append(msg)
         rs.append(r)
-    fake = tc.encrypt(pks.public_key(), b"X marks the spot", tc.fr_rand(r_rng))  # tests/honey_badger.rs:90
+    fake = tc.encrypt(pks.public_key(), b"X marks the spot", tc.fr_rand(r_rng), digest)  # tests/honey_badger.rs:90
     enc_u = [bls.g1_compress(c[0]) for c in honest]
     enc_w = [bls.g2_compress(c[2]) for c in honest]
     wire_u, wire_w = list(enc_u), list(enc_w)
@@ -140,7 +142,7 @@ def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool):
             hashes.append(None)
             continue
         ct = (u, v_bytes[j], w)
-        h = tc.hash_g1_g2(u, v_bytes[j])
+        h = tc.hash_g1_g2(u, v_bytes[j], digest)
         cts.append(ct)
         hashes.append(h)
         ct_status.append(CT_VALID if tc.ciphertext_verify(ct, hash_pt=h) else CT_INVALID)
@@ -221,7 +223,7 @@ def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool):
                 continue
             pts = [(i, (bls.g1_mul(cts[j][0], sk_shares[me]) if (own and i == me) else share_pt[(j, i)]))
                    for i in idx[:t]]
-            pt = tc.decrypt(pks, pts, cts[j])
+            pt = tc.decrypt(pks, pts, cts[j], digest)
             if j != ident_ct:
                 assert pt == msgs[j]
             plains.append(pt)
@@ -247,7 +249,7 @@ def make_epoch(n: int, p: int, v_lens, edge: bool, corrupt_every: int, pool):
         return out
 
     d = dict(
-        digest=np.array("sha256"), n=np.int64(n), t=np.int64(t),
+        digest=np.array(digest), n=np.int64(n), t=np.int64(t),
         pk_comp=np.stack([np.frombuffer(bls.g1_compress(q), dtype=np.uint8) for q in pk_shares]),
         master_pk=np.frombuffer(bls.g1_compress(pks.public_key()), dtype=np.uint8),
         u=np.stack([np.frombuffer(x, dtype=np.uint8) for x in wire_u]),
@@ -289,8 +291,8 @@ def main():
     names = sys.argv[1:] or list(FIXTURES)
     with mp.Pool(min(8, os.cpu_count() or 1)) as pool:
         for name in names:
-            n, p, v_lens, edge, ce = FIXTURES[name]
-            d = make_epoch(n, p, v_lens, edge, ce, pool)
+            n, p, v_lens, edge, ce, *dg = FIXTURES[name]
+            d = make_epoch(n, p, v_lens, edge, ce, pool, *dg)
             path = os.path.join(HERE, f"{name}.npz")
             np.savez_compressed(path, **d)
             st = d["expect_share_status"]

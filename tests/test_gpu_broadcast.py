@@ -174,3 +174,101 @@ def test_broadcast_decode(hbx_ctx, n, value):
             assert st[i] == 0, (i, st[i])
             assert out[i, : out_len[i]].tobytes() == want
     assert st[0] == 0 and out[0, : out_len[0]].tobytes() == value
+
+
+# ---- Merkle tree build + gen_proof and the SHA3
+# variant (HBX_MERKLE_SHA3: later hbbft's src/broadcast/merkle.rs; north_star "SHA3 Merkle") ----
+def _set_merkle(ctx, variant):
+    from hbbft_amd.hbx import MERKLE_SHA3, MERKLE_SHA256
+
+    ctx.set_merkle_digest(MERKLE_SHA3 if variant == "sha3" else MERKLE_SHA256)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["sha256", "sha3"])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 7, 13, 128, 256])
+def test_merkle_build_and_gen_proof(hbx_ctx, n, variant):
+    """Every level of the tree, and gen_proof for every leaf, byte-identical with the oracle's
+    MerkleTree / gen_proof (odd node promoted; proofs in hbx_merkle_validate_d's format), and every
+    generated proof validates."""
+    _set_merkle(hbx_ctx, variant)
+    rng = np.random.default_rng(n * 31 + len(variant))
+    inst, L = 2, 37
+    shards = rng.integers(0, 256, size=(inst, n, L), dtype=np.uint8)
+    cnt = hbx_ctx.merkle_node_count(n)
+    nodes = torch.zeros((inst, cnt, 32), dtype=torch.uint8, device="cuda")
+    roots = torch.zeros((inst, 32), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_build_d(dev(shards), nodes, roots)
+    req = np.array([(i, j) for i in range(inst) for j in range(n)], dtype=np.uint32)
+    P = len(req)
+    nh = torch.zeros((P, 17, 32), dtype=torch.uint8, device="cuda")
+    sh = torch.zeros((P, 16, 32), dtype=torch.uint8, device="cuda")
+    sides = torch.zeros(P, dtype=torch.int32, device="cuda")
+    depth = torch.zeros(P, dtype=torch.int32, device="cuda")
+    proot = torch.zeros((P, 32), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_proofs_d(nodes, n, dev(req), nh, sh, sides, depth, proot)
+    torch.cuda.synchronize()
+    nodes, roots = nodes.cpu().numpy(), roots.cpu().numpy()
+    proofs, senders = [], []
+    for i in range(inst):
+        leaves = [bytes([j & 0xFF]) + shards[i, j].tobytes() for j in range(n)]
+        tree = rm.MerkleTree(leaves, variant)
+        flat = [h for lvl in tree.levels for h in lvl]
+        assert len(flat) == cnt
+        assert [bytes(x) for x in nodes[i]] == flat
+        assert roots[i].tobytes() == tree.root_hash()
+        for j in range(n):
+            proofs.append(tree.gen_proof(leaves[j]))
+            senders.append(j)
+    want = flatten(proofs, senders)
+    _, w_nodes, w_sibs, w_sides, w_depth, w_roots, _ = want
+    np.testing.assert_array_equal(depth.cpu().numpy(), w_depth.astype(np.int32))
+    np.testing.assert_array_equal(sides.cpu().numpy(), w_sides.astype(np.int32))
+    np.testing.assert_array_equal(proot.cpu().numpy(), w_roots)
+    got_n, got_s = nh.cpu().numpy(), sh.cpu().numpy()
+    for q in range(P):
+        d = int(w_depth[q])
+        np.testing.assert_array_equal(got_n[q, :d + 1], w_nodes[q, :d + 1])
+        np.testing.assert_array_equal(got_s[q, :d], w_sibs[q, :d])
+    valid = torch.zeros(P, dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_validate_d(dev(want[0]), nh, sh, sides, depth, proot, dev(want[6]), n, valid)
+    torch.cuda.synchronize()
+    assert valid.cpu().numpy().all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 13])
+def test_merkle_sha3_validate_and_decode(hbx_ctx, n):
+    """The SHA3 variant through validate_proof (bad sender / value / root rejected) and
+    decode_from_shards (f silent, wrong root)."""
+    _set_merkle(hbx_ctx, "sha3")
+    value = bytes(range(256)) * 2
+    shards, leaves, tree = rm.send_shards(value, n, "sha3")
+    proofs, senders = [], []
+    for i, leaf in enumerate(leaves):
+        p = tree.gen_proof(leaf)
+        proofs += [p, p, dict(p, value=p["value"][:-1] + bytes([p["value"][-1] ^ 1])), dict(p, root_hash=b"\x11" * 32)]
+        senders += [i, (i + 1) % n, i, i]
+    arrs = flatten(proofs, senders)
+    valid = torch.zeros(len(proofs), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_validate_d(*[dev(a) for a in arrs], n, valid)
+    torch.cuda.synchronize()
+    want = [rm.validate_broadcast_proof(p, s, n, "sha3") for p, s in zip(proofs, senders)]
+    assert valid.cpu().numpy().astype(bool).tolist() == want and sum(want) == n
+    f = rm.num_faulty(n)
+    k, m = rm.coding_counts(n)
+    L = shards.shape[1]
+    buf = np.stack([shards] * 2)
+    present = np.ones((2, n), dtype=np.uint8)
+    present[:, n - f:] = 0
+    buf[present == 0] = 0
+    roots = np.stack([np.frombuffer(tree.root_hash(), dtype=np.uint8)] * 2).copy()
+    roots[1, 3] ^= 1
+    out = torch.zeros((2, k * L), dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(2, dtype=torch.int64, device="cuda")
+    st = torch.zeros(2, dtype=torch.int32, device="cuda")
+    hbx_ctx.broadcast_decode_d(dev(buf), dev(present), dev(roots), k, m, out, out_len, st)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert st[0] == 0 and out[0, : int(out_len[0])].cpu().numpy().tobytes() == value
+    assert st[1] == HBX_E_ROOT_MISMATCH

@@ -12,7 +12,14 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def _load(n):
-    return dict(np.load(os.path.join(GOLDEN, f"coin_n{n}.npz"), allow_pickle=False))
+    name = n if isinstance(n, str) else f"coin_n{n}"
+    return dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+
+
+def _digest(ctx, d):
+    from hbbft_amd.hbx import DIGEST_SHA3_256, DIGEST_SHA256
+
+    ctx.set_digest(DIGEST_SHA3_256 if str(d.get("digest", "sha256")) == "sha3_256" else DIGEST_SHA256)
 
 
 def _nonces(d):
@@ -21,9 +28,10 @@ def _nonces(d):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7, 128])
+@pytest.mark.parametrize("n", [4, 7, 128, "coin_n4_sha3"])
 def test_coin_matches_golden(hbx_ctx, n):
     d = _load(n)
+    _digest(hbx_ctx, d)
     assert (hbx_ctx.set_pk_shares([r.tobytes() for r in d["pk_comp"]]) == 0).all()
     h = hbx_ctx.prepare_nonces(_nonces(d))
     np.testing.assert_array_equal(h, d["h"])
@@ -41,9 +49,10 @@ def test_coin_matches_golden(hbx_ctx, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 128])
+@pytest.mark.parametrize("n", [4, 128, "coin_n4_sha3"])
 def test_sign_matches_honest_shares(hbx_ctx, n):
     d = _load(n)
+    _digest(hbx_ctx, d)
     hbx_ctx.prepare_nonces(_nonces(d))
     sigs = hbx_ctx.sign(d["sk"])
     honest = d["expect_valid"]
@@ -64,6 +73,27 @@ def test_hash_g2_many_nonces_vs_oracle(hbx_ctx):
     rnd = random.Random(2024)
     lens = [0, 1, 32, 63, 64, 65, 128, 1100] + [rnd.randrange(0, 1100) for _ in range(248)]
     msgs = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
+    _digest(hbx_ctx, {})
     h = hbx_ctx.prepare_nonces(msgs)
     for j, m in enumerate(msgs):
         assert bytes(h[j]) == bls.g2_compress(tc.hash_g2(m)), f"message {j} (len {len(m)})"
+
+
+@pytest.mark.gpu
+def test_hash_g2_sha3_digest_vs_oracle(hbx_ctx):
+    """hash_g2 under DIGEST = SHA3-256 (hbx_set_digest): 64 messages vs the oracle."""
+    import random
+
+    from hbbft_amd.hbx import DIGEST_SHA256, DIGEST_SHA3_256
+    from oracle import bls12_381 as bls
+    from oracle import threshold as tc
+
+    rnd = random.Random(77)
+    msgs = [bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 400))) for _ in range(64)]
+    hbx_ctx.set_digest(DIGEST_SHA3_256)
+    try:
+        h = hbx_ctx.prepare_nonces(msgs)
+    finally:
+        hbx_ctx.set_digest(DIGEST_SHA256)
+    for j, m in enumerate(msgs):
+        assert bytes(h[j]) == bls.g2_compress(tc.hash_g2(m, "sha3_256")), j

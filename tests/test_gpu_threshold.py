@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-FIXTURES = ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256"]
+FIXTURES = ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256", "hb_epoch_n7_sha3"]
 
 
 def _load(name):
@@ -30,6 +30,10 @@ def _check_plain(d, j, pt: bytes, own=False):
 
 
 def _set_keys(ctx, d):
+    """Era keys plus the fixture's DIGEST variant (hbx_set_digest)."""
+    from hbbft_amd.hbx import DIGEST_SHA3_256, DIGEST_SHA256
+
+    ctx.set_digest(DIGEST_SHA3_256 if str(d["digest"]) == "sha3_256" else DIGEST_SHA256)
     st = ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]])
     assert (st == 0).all()
 
@@ -38,7 +42,6 @@ def _set_keys(ctx, d):
 @pytest.mark.parametrize("name", FIXTURES)
 def test_epoch_matches_golden(hbx_ctx, name):
     d = _load(name)
-    assert str(d["digest"]) == "sha256"
     _set_keys(hbx_ctx, d)
     p, n = d["shares"].shape[:2]
     ct_ok = hbx_ctx.prepare_ciphertexts(_cts(d))
@@ -132,6 +135,7 @@ def test_unknown_sender_status(hbx_ctx):
     Err(UnknownSender), honey_badger.rs:64-66), never a verification."""
     d = _load("hb_epoch_n7")
     n = d["shares"].shape[1]
+    _set_keys(hbx_ctx, d)
     hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"][: n - 2]])
     p = d["shares"].shape[0]
     hbx_ctx.prepare_ciphertexts(_cts(d))
@@ -178,10 +182,11 @@ def test_public_keys_match_oracle(hbx_ctx, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n10", "hb_cols_n256"])
+@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n10", "hb_cols_n256", "hb_epoch_n7_sha3"])
 def test_encrypt_matches_oracle(hbx_ctx, name):
     """PublicKey::encrypt with given r_j: U, V, W bytes equal the oracle's (honey_badger.rs:116)."""
     d = _load(name)
+    _set_keys(hbx_ctx, d)
     off = d["enc_msg_off"]
     p = len(off) - 1
     msgs = [d["enc_msg_blob"][int(off[j]):int(off[j + 1])].tobytes() for j in range(p)]

@@ -85,6 +85,23 @@ def test_fq_mul_lazy_range(hc):
         assert r % bls.P == a * b * rinv % bls.P, (hex(a), hex(b))
 
 
+def test_fq_sqr_lazy_range(hc):
+    """The dedicated square (105 + 196 digit products) equals the product of a with itself on lazy
+    operands in [0, 2p], output < 2p."""
+    rnd = random.Random(11)
+    P2 = 2 * bls.P
+    vals = [0, 1, 2, bls.P - 1, bls.P, bls.P + 1, P2 - 1, P2, (1 << 381) - 1, (1 << 380) + 12345]
+    vals += [rnd.randrange(P2 + 1) for _ in range(600)]
+    rinv = pow(1 << 384, -1, bls.P)
+    for a in vals:
+        A = (ctypes.c_uint32 * 12)(*[(a >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        O = (ctypes.c_uint32 * 12)()
+        hc.hc_fq_sqr_raw(A, O)
+        r = sum(int(O[i]) << (32 * i) for i in range(12))
+        assert r < P2, hex(a)
+        assert r % bls.P == a * a * rinv % bls.P, hex(a)
+
+
 def test_point_roundtrips(hc):
     for k in (1, 2, 0xDEADBEEF, bls.R - 1):
         c1 = bls.g1_compress(bls.g1_mul(bls.G1_GEN, k))
@@ -117,6 +134,28 @@ def test_sha256_and_hash_g1_g2(hc):
         out = ctypes.create_string_buffer(96)
         assert hc.hc_hash_g1_g2(bls.g1_compress(u), v, len(v), out) == 0
         assert out.raw == bls.g2_compress(tc.hash_g1_g2(u, v))
+
+
+def test_sha3_256_and_digest_switch(hc):
+    """Keccak-f[1600] SHA3-256 (the opt-in DIGEST) vs hashlib, every padding
+    boundary of the 136-byte rate, and hash_g1_g2 under DIGEST = SHA3-256 vs the oracle."""
+    hc.hc_sha3_256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    hc.hc_sha3_256_2.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    hc.hc_hash_g1_g2_v.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p]
+    rnd = random.Random(3)
+    for n in (0, 1, 31, 135, 136, 137, 271, 272, 273, 1000):
+        m = bytes(rnd.getrandbits(8) for _ in range(n))
+        out = ctypes.create_string_buffer(32)
+        hc.hc_sha3_256(m, len(m), out)
+        assert out.raw == hashlib.sha3_256(m).digest(), n
+        k = n // 3
+        hc.hc_sha3_256_2(m[:k], k, m[k:], n - k, out)
+        assert out.raw == hashlib.sha3_256(m).digest(), n
+    u = bls.g1_mul(bls.G1_GEN, 91)
+    for v in (b"", b"x" * 64, b"y" * 65, b"z" * 300):
+        out = ctypes.create_string_buffer(96)
+        assert hc.hc_hash_g1_g2_v(bls.g1_compress(u), v, len(v), 1, out) == 0
+        assert out.raw == bls.g2_compress(tc.hash_g1_g2(u, v, "sha3_256"))
 
 
 def test_g2_clear_cofactor_psi(hc):

@@ -1,12 +1,19 @@
-"""Multi-rank epoch sharding on CPU (gloo, world_size 2): each rank fills its proposer-column
-slab, one all-gather assembles the node's full epoch result."""
+"""Multi-rank epoch sharding on CPU (gloo): each rank owns a block of proposer columns of the
+N = 64 fixture (tests/golden/hb_epoch_n64.npz, BASELINE config 2), fills its result slab with that
+slice's per-share / per-ciphertext / combine statuses (the oracle's results for the slice, which
+is what the engine returns for it: test_gpu_shard_slices checks that on the GPU), and one
+all-gather assembles the node's full epoch result.  World sizes 2 and 3 (N not
+divisible by the world size)."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+FIX = os.path.join(os.path.dirname(__file__), "golden", "hb_epoch_n64.npz")
 
 
 def _free_port():
@@ -17,37 +24,97 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n, q):
+def slab_for_slice(d, n, world, rank, share_status=None, ct_status=None, comb_status=None):
+    from hbbft_amd import shard
+
+    lo, hi = shard.proposer_range(n, world, rank)
+    pj = hi - lo
+    lay = shard.slab_layout(n, shard.max_columns(n, world))
+    slab = np.zeros(lay["size"], dtype=np.uint8)
+    ss = d["expect_share_status"][lo:hi] if share_status is None else share_status
+    cs = d["expect_ct_status"][lo:hi] if ct_status is None else ct_status
+    st = d["expect_status"][lo:hi] if comb_status is None else comb_status
+    slab[lay["valid"][0]:lay["valid"][0] + pj * n] = np.asarray(ss, dtype=np.uint8).reshape(-1)
+    slab[lay["ct_valid"][0]:lay["ct_valid"][0] + pj] = cs
+    slab[lay["status"][0]:lay["status"][0] + 4 * pj] = np.asarray(st, dtype=np.int32).view(np.uint8)
+    return slab
+
+
+def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from hbbft_amd import shard
 
-    lo, hi = shard.proposer_range(n, world, rank)
-    pj = hi - lo
-    lay = shard.slab_layout(n, pj)
-    slab = torch.zeros(lay["size"], dtype=torch.uint8)
-    full_valid = (np.arange(n * n).reshape(n, n) % 5) != 0
-    slab[lay["valid"][0]:lay["valid"][1]] = torch.from_numpy(full_valid[lo:hi].astype(np.uint8).reshape(-1))
-    slab[lay["ct_valid"][0]:lay["ct_valid"][1]] = 1
-    st = np.arange(lo, hi, dtype=np.int32) * -1
-    slab[lay["status"][0]:lay["status"][1]] = torch.from_numpy(st.view(np.uint8))
+    d = dict(np.load(FIX, allow_pickle=False))
+    n = int(d["n"])
+    slab = torch.from_numpy(slab_for_slice(d, n, world, rank))
     g = shard.all_gather_slabs(slab, world)
-    valid, ctv, status = shard.assemble(g.numpy(), n, world)
-    ok = (valid == full_valid).all() and ctv.all() and (status == -np.arange(n)).all()
+    ss, cs, st = shard.assemble(g.numpy(), n, world)
+    ok = ((ss == d["expect_share_status"]).all() and (cs == d["expect_ct_status"]).all()
+          and (st == d["expect_status"]).all())
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
 
-def test_two_rank_gather():
-    world, n = 2, 8
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_gather_fixture_epoch(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    assert res == {r: True for r in range(world)}
+
+
+def test_proposer_ranges_cover():
+    from hbbft_amd import shard
+
+    for n in (1, 7, 64, 256):
+        for world in (1, 2, 3, 8):
+            rs = [shard.proposer_range(n, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(h - l for l, h in rs) == shard.max_columns(n, world)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [3, 8])
+def test_gpu_shard_slices(hbx_ctx, world):
+    """The sharded result path with the HIP engine: each rank's proposer slice of the N = 64 epoch
+    is run through hbx_decrypt_epoch_d on its own (as that rank's GPU would), the slabs are
+    assembled as the all-gather would, and the node's epoch result equals the full fixture."""
+    from hbbft_amd import shard
+
+    d = dict(np.load(FIX, allow_pickle=False))
+    n = int(d["n"])
+    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
+    dev = torch.device("cuda", 0)
+    slabs = []
+    for r in range(world):
+        lo, hi = shard.proposer_range(n, world, r)
+        pj = hi - lo
+        off = d["v_off"][lo:hi + 1].astype(np.int64)
+        off0 = off - off[0]
+        t_u = torch.from_numpy(np.ascontiguousarray(d["u"][lo:hi])).to(dev)
+        t_w = torch.from_numpy(np.ascontiguousarray(d["w"][lo:hi])).to(dev)
+        t_v = torch.from_numpy(np.ascontiguousarray(d["v_blob"][off[0]:off[-1]])).to(dev)
+        t_off = torch.from_numpy(off0).to(dev)
+        t_sh = torch.from_numpy(np.ascontiguousarray(d["shares"][lo:hi])).to(dev)
+        t_pr = torch.from_numpy(np.ascontiguousarray(d["present"][lo:hi]).astype(np.uint8)).to(dev)
+        t_out = torch.zeros(max(int(off0[-1]), 1), dtype=torch.uint8, device=dev)
+        t_valid = torch.zeros(pj * n, dtype=torch.uint8, device=dev)
+        t_ct = torch.zeros(pj, dtype=torch.uint8, device=dev)
+        t_st = torch.zeros(pj, dtype=torch.int32, device=dev)
+        hbx_ctx.decrypt_epoch_d(t_u, t_v, t_off, t_w, pj, int(np.max(np.diff(off0))), t_sh, n, int(d["t"]), t_out,
+                                d_valid=t_valid, d_ct_valid=t_ct, d_status=t_st, d_present=t_pr)
+        slabs.append(slab_for_slice(d, n, world, r, t_valid.cpu().numpy().reshape(pj, n), t_ct.cpu().numpy(),
+                                    t_st.cpu().numpy()))
+    ss, cs, st = shard.assemble(np.stack(slabs), n, world)
+    np.testing.assert_array_equal(ss, d["expect_share_status"])
+    np.testing.assert_array_equal(cs, d["expect_ct_status"])
+    np.testing.assert_array_equal(st, d["expect_status"])

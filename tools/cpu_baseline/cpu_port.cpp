@@ -87,4 +87,83 @@ int cpu_verify_dec_shares(const uint8_t* pk48, uint32_t n, const uint8_t* u48, c
   for (auto& th : pool) th.join();
   return 0;
 }
+
+// CPU baseline row (b) of BASELINE.md §2: the same verify_decryption_share bits computed the way
+// a CPU implementation would batch them -- H_j = hash_g1_g2(U_j, V_j) hoisted to once per proposer
+// (with its Miller lines prepared once, like the kernels' k_prepare_lines), and each share checked
+// as e(S, H_j) e(-pk_i, W_j) == 1 with ONE two-pair Miller loop and ONE final exponentiation.
+// jobs are (proposer, sender) pairs; the per-proposer preparation of every proposer the jobs touch
+// is included in the time (it is part of the work), spread over the same threads.
+int cpu_verify_dec_shares_fused(const uint8_t* pk48, uint32_t n, const uint8_t* u48, const uint8_t* v_blob,
+                                const uint64_t* v_off, const uint8_t* w96, const uint8_t* shares48, uint32_t p,
+                                const uint32_t* jobs, uint32_t njobs, int threads, uint8_t* out) {
+  if (threads < 1) threads = 1;
+  struct prep {
+    bool used = false, ok = false, h_inf = false, w_inf = false;
+    std::vector<line_pre> lh, lw;
+  };
+  std::vector<prep> P(p);
+  for (uint32_t k = 0; k < njobs; k++) P[jobs[2 * k]].used = true;
+  std::vector<uint32_t> props;
+  for (uint32_t j = 0; j < p; j++)
+    if (P[j].used) props.push_back(j);
+  auto ok1 = [](int st) { return st == HBX_PT_OK || st == HBX_PT_INFINITY; };
+  {
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+      for (;;) {
+        const uint32_t q = next.fetch_add(1);
+        if (q >= props.size()) return;
+        const uint32_t j = props[q];
+        prep& pr = P[j];
+        g1a U;
+        g2a W;
+        if (!ok1(g1_decompress(u48 + (size_t)j * 48, U)) || !ok1(g2_decompress(w96 + (size_t)j * 96, W))) continue;
+        uint8_t d[32];
+        hash_g1_g2_digest(u48 + (size_t)j * 48, v_blob + v_off[j], v_off[j + 1] - v_off[j], d);
+        const g2a H = g2_to_affine(hash_g2_from_digest(d));
+        pr.lh.resize(MILLER_LINES);
+        pr.lw.resize(MILLER_LINES);
+        fq2 scratch[2 * MILLER_LINES];
+        pr.h_inf = H.inf;
+        pr.w_inf = W.inf;
+        if (!H.inf) g2_prepare_lines(H, pr.lh.data(), scratch);
+        if (!W.inf) g2_prepare_lines(W, pr.lw.data(), scratch);
+        pr.ok = true;
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+  }
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const uint32_t k = next.fetch_add(1);
+      if (k >= njobs) return;
+      const uint32_t j = jobs[2 * k], i = jobs[2 * k + 1];
+      const prep& pr = P[j];
+      g1a pk, S;
+      if (!pr.ok || !ok1(g1_decompress(pk48 + (size_t)i * 48, pk)) ||
+          !ok1(g1_decompress(shares48 + ((size_t)j * n + i) * 48, S))) {
+        out[k] = 0;
+        continue;
+      }
+      pk.y = fq_neg(pk.y);
+      const bool useA = !S.inf && !pr.h_inf, useB = !pk.inf && !pr.w_inf;
+      if (!useA && !useB) {
+        out[k] = 1;
+        continue;
+      }
+      const fq12 f = miller_loop2(pr.lh.data(), S, useA, pr.lw.data(), pk, useB);
+      out[k] = fq12_is_one(final_exponentiation(f)) ? 1 : 0;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; t++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return 0;
+}
 }

@@ -19,6 +19,12 @@ void hc_fq_mul_raw(const uint32_t* a, const uint32_t* b, uint32_t* out) {
   const fq r = fq_mul(x, y);
   for (int i = 0; i < 12; i++) out[i] = r.l[i];
 }
+void hc_fq_sqr_raw(const uint32_t* a, uint32_t* out) {
+  fq x;
+  for (int i = 0; i < 12; i++) x.l[i] = a[i];
+  const fq r = fq_sqr(x);
+  for (int i = 0; i < 12; i++) out[i] = r.l[i];
+}
 // subgroup checks on raw affine coordinates (canonical big-endian; G2 as x.c1||x.c0||y.c1||y.c0):
 // 1 = in G1/G2, 0 = not, -1 = not on the curve
 int hc_g1_torsion_free(const uint8_t* x48, const uint8_t* y48) {
@@ -118,8 +124,17 @@ int hc_g2_mul_cofactor(const uint8_t* in96, uint8_t* out96) {
 }
 extern "C" {
 void hc_sha256(const uint8_t* m, uint64_t n, uint8_t* out32) { sha256_2(m, n, nullptr, 0, out32); }
+void hc_sha3_256(const uint8_t* m, uint64_t n, uint8_t* out32) { sha3_256_2(m, n, nullptr, 0, out32); }
+// two-range form (the split point exercises the concatenation path)
+void hc_sha3_256_2(const uint8_t* m0, uint64_t n0, const uint8_t* m1, uint64_t n1, uint8_t* out32) {
+  sha3_256_2(m0, n0, m1, n1, out32);
+}
 int hc_hash_g1_g2(const uint8_t* u48, const uint8_t* v, uint64_t vlen, uint8_t* out96) {
   g2j h = hash_g1_g2(u48, v, vlen);
+  g2_compress(g2_to_affine(h), out96); return 0;
+}
+int hc_hash_g1_g2_v(const uint8_t* u48, const uint8_t* v, uint64_t vlen, int variant, uint8_t* out96) {
+  g2j h = hash_g1_g2(u48, v, vlen, variant);
   g2_compress(g2_to_affine(h), out96); return 0;
 }
 int hc_hash_g2_digest(const uint8_t* d32, uint8_t* out96) {
