@@ -333,7 +333,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u32 (Fq 12x32-bit Montgomery limbs)",
         "data": "synthetic (seeded keys, 1 KiB random contributions, GPU-made ciphertexts/shares, 1/64 foreign-ciphertext shares)",
