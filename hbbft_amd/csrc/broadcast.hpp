@@ -101,6 +101,110 @@ __global__ void __launch_bounds__(256) k_rs_code(uint8_t* __restrict__ shards, s
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// GF(2^8) coding by byte permutes.  Multiplication by a fixed coefficient c is GF(2)-linear, so
+// c * d = c * (d & 0x07) ^ c * (d & 0x38) ^ c * (d & 0xC0): three lookups in tables of 8, 8 and 4
+// bytes, and an 8-byte table is exactly what one v_perm_b32 selects from (selector bytes 0..7
+// over two dwords) -- for four packed data bytes at once.  Per (output, input) coefficient and
+// data dword: 3 perms and 1.5 xors (v_xor3), no LDS, no per-byte work.  The 32-byte table of a
+// coefficient is wave-uniform (one s_load_dwordx8); the two 8-byte tables need VGPR copies
+// (one constant-bus operand per VALU op), which D data dwords per lane share.  The selector
+// words depend on the data only and are computed once per input dword.
+// tables: u32[jobs][RS_MAX_N][k][8] = {T0 lo, T0 hi, T1 lo, T1 hi, T2, 0, 0, 0}, T0[i] = c*i,
+// T1[i] = c*(i << 3) (i < 8), T2[i] = c*(i << 6) (i < 4).
+// ---------------------------------------------------------------------------------------------
+struct alignas(32) gf_ptab {
+  uint32_t w[8];
+};
+
+// Perm tables for per-instance jobs (reconstruct): one lane per coefficient of jobs[inst]
+// (logs in coef, GF_COEF_ZERO = 0).  grid (ceil(RS_MAX_N * k / 256), inst).
+__global__ void __launch_bounds__(256) k_rs_perm_tables(const rs_job* __restrict__ jobs, const uint16_t* __restrict__ coef,
+                                                        uint32_t k, const uint16_t* __restrict__ glog,
+                                                        const uint8_t* __restrict__ gexp, gf_ptab* __restrict__ tables) {
+  __shared__ gf_tab T;
+  gf_stage(T, glog, gexp);
+  __syncthreads();
+  const uint32_t inst = blockIdx.y;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t no = (uint32_t)jobs[inst].n_out;
+  if (e >= no * k) return;
+  const uint16_t lc = coef[(size_t)inst * RS_MAX_N * k + e];
+  uint8_t b[20];
+  for (int i = 0; i < 8; i++) {
+    b[i] = lc == GF_COEF_ZERO || i == 0 ? 0 : T.ex[T.lg[i] + lc];
+    b[8 + i] = lc == GF_COEF_ZERO || i == 0 ? 0 : T.ex[T.lg[i << 3] + lc];
+  }
+  for (int i = 0; i < 4; i++) b[16 + i] = lc == GF_COEF_ZERO || i == 0 ? 0 : T.ex[T.lg[i << 6] + lc];
+  gf_ptab t;
+  for (int w = 0; w < 5; w++)
+    t.w[w] = (uint32_t)b[4 * w] | ((uint32_t)b[4 * w + 1] << 8) | ((uint32_t)b[4 * w + 2] << 16) |
+             ((uint32_t)b[4 * w + 3] << 24);
+  t.w[5] = t.w[6] = t.w[7] = 0;
+  tables[(size_t)inst * RS_MAX_N * k + e] = t;
+}
+
+// out rows = XOR_c coef[o][c] * in rows c, byte columns; needs L % 4 == 0 (dword rows).  A wave
+// covers 64 * D consecutive dwords of every row (lane l: dwords l, l + 64, ...), accumulating CH
+// output rows per pass over the inputs.  grid (ceil(L / (4 * 256 * D)), inst); job_stride as
+// k_rs_code (0: all instances run job 0 with tables[0], 1: per-instance jobs and tables).
+template <int CH, int D>
+__global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
+                                                      uint32_t k, const rs_job* __restrict__ jobs,
+                                                      const gf_ptab* __restrict__ tables, uint32_t job_stride) {
+  const uint32_t inst = blockIdx.y;
+  const rs_job* J = jobs + (size_t)inst * job_stride;
+  const int no = ld_uniform(&J->n_out);
+  const uint32_t Ld = L >> 2;
+  const uint32_t wave0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * D;
+  if (no == 0 || wave0 >= Ld) return;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t* base = reinterpret_cast<uint32_t*>(shards + (size_t)inst * inst_stride);
+  const gf_ptab* tb = tables + (size_t)inst * job_stride * RS_MAX_N * k;
+  bool ok[D];
+#pragma unroll
+  for (int j = 0; j < D; j++) ok[j] = wave0 + lane + 64 * j < Ld;
+  for (int o0 = 0; o0 < no; o0 += CH) {
+    uint32_t acc[CH][D];
+#pragma unroll
+    for (int o = 0; o < CH; o++)
+#pragma unroll
+      for (int j = 0; j < D; j++) acc[o][j] = 0;
+#pragma unroll 1
+    for (uint32_t c = 0; c < k; c++) {
+      const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c]) * Ld + wave0 + lane;
+      uint32_t s0[D], s1[D], s2[D];
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        const uint32_t d = ok[j] ? src[64 * j] : 0u;
+        s0[j] = d & 0x07070707u;
+        s1[j] = (d >> 3) & 0x07070707u;
+        s2[j] = (d >> 6) & 0x03030303u;
+      }
+      const gf_ptab* t = tb + c;
+#pragma unroll
+      for (int o = 0; o < CH; o++) {
+        if (o0 + o < no) {
+          const gf_ptab T = ld_uniform(t + (size_t)(o0 + o) * k);
+#pragma unroll
+          for (int j = 0; j < D; j++)
+            acc[o][j] ^= __builtin_amdgcn_perm(T.w[1], T.w[0], s0[j]) ^ __builtin_amdgcn_perm(T.w[3], T.w[2], s1[j]) ^
+                         __builtin_amdgcn_perm(0u, T.w[4], s2[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CH; o++) {
+      if (o0 + o < no) {
+        uint32_t* dst = base + (size_t)ld_uniform(&J->out_idx[o0 + o]) * Ld + wave0 + lane;
+#pragma unroll
+        for (int j = 0; j < D; j++)
+          if (ok[j]) dst[64 * j] = acc[o][j];
+      }
+    }
+  }
+}
+
 // reconstruct_shards set-up, one block per instance (reed-solomon-erasure 3.1.0):
 // first k present shards -> invert that k x k sub-matrix of the encoding matrix (Gauss-Jordan in
 // LDS) -> job 0: rebuild missing data shards from the k sub shards; job 1: re-encode missing

@@ -37,6 +37,19 @@ extern unsigned long long hbx_opcount_fqmul;
 
 namespace hbx {
 
+// Load of read-only data at a wave-uniform address through the constant address space, so it
+// is issued as scalar (SMEM) loads through the scalar cache: a plain global load after an
+// out-of-line call cannot be proven unclobbered and would be a vector load per lane.
+template <class T>
+HBX_HD T ld_uniform(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(4))) const T* cptr;
+  return *(cptr)p;
+#else
+  return *p;
+#endif
+}
+
 struct fq {
   uint32_t l[12];
 };

@@ -19,6 +19,10 @@ using namespace hbx;
 
 namespace {
 
+// one wave per SIMD: a one-lane-per-check launch with fewer waves leaves SIMDs idle, and the
+// three-lane kernel finishes it sooner (MI355X: 256 CUs x 4 SIMDs)
+constexpr int VERIFY_FILL_WAVES = 1024;
+
 struct dbuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -51,6 +55,7 @@ struct hbx_ctx {
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
+  int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1 or 3 lanes per share check
   // era state
   uint32_t n_keys = 0;
   dbuf pk, pk_status, pk_comp;
@@ -76,7 +81,7 @@ struct hbx_ctx {
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
   dbuf gf_log, gf_exp;
   uint32_t rs_k = 0, rs_m = 0;
-  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, roots;
+  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, roots;
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
@@ -207,6 +212,37 @@ static const gf_host& gf() {
   return g;
 }
 
+// Byte-permute tables of one coefficient (layout in broadcast.hpp, k_rs_code_perm).
+static gf_ptab gf_perm_table(uint8_t c) {
+  const gf_host& g = gf();
+  uint8_t b[20];
+  for (int i = 0; i < 8; i++) {
+    b[i] = g.mul(c, (uint8_t)i);
+    b[8 + i] = g.mul(c, (uint8_t)(i << 3));
+  }
+  for (int i = 0; i < 4; i++) b[16 + i] = g.mul(c, (uint8_t)(i << 6));
+  gf_ptab t{};
+  for (int w = 0; w < 5; w++)
+    t.w[w] = (uint32_t)b[4 * w] | ((uint32_t)b[4 * w + 1] << 8) | ((uint32_t)b[4 * w + 2] << 16) |
+             ((uint32_t)b[4 * w + 3] << 24);
+  return t;
+}
+
+// One coding pass: the byte-permute kernel when rows are whole dwords, else the LDS log/exp one.
+static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, uint32_t k, uint32_t inst,
+                    const rs_job* jobs, const uint16_t* coef, const gf_ptab* ptab, uint32_t job_stride, hipStream_t s) {
+  timed t_(c, HBX_K_RS_CODE, s);
+  if (L % 4 == 0) {
+    constexpr int CH = 48, D = 2;
+    const uint32_t Ld = L / 4;
+    const dim3 grid((Ld + 256 * D - 1) / (256 * D), inst);
+    hipLaunchKernelGGL((k_rs_code_perm<CH, D>), grid, dim3(256), 0, s, d_shards, stride, L, k, jobs, ptab, job_stride);
+  } else {
+    hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, stride, L, k, jobs, coef,
+                       job_stride, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  }
+}
+
 // Encoding matrix V * inverse(V[0..k]) with V[r][c] = r^c ((k + m) x k, reed-solomon-erasure 3.1.0).
 static bool rs_matrix(uint32_t k, uint32_t m, std::vector<uint8_t>& out) {
   const gf_host& g = gf();
@@ -263,8 +299,13 @@ static int rs_setup(hbx_ctx* c, uint32_t k, uint32_t m, hipStream_t s) {
       const uint8_t v = M[(size_t)(k + o) * k + q];
       coef[(size_t)o * k + q] = v ? gf().lg[v] : GF_COEF_ZERO;
     }
-  if (!c->rs_enc.ensure(M.size()) || !c->rs_enc_job.ensure(sizeof(rs_job)) || !c->rs_enc_coef.ensure(coef.size() * 2))
+  std::vector<gf_ptab> ptab((size_t)m * k);
+  for (uint32_t o = 0; o < m; o++)
+    for (uint32_t q = 0; q < k; q++) ptab[(size_t)o * k + q] = gf_perm_table(M[(size_t)(k + o) * k + q]);
+  if (!c->rs_enc.ensure(M.size()) || !c->rs_enc_job.ensure(sizeof(rs_job)) || !c->rs_enc_coef.ensure(coef.size() * 2) ||
+      !c->rs_enc_ptab.ensure(ptab.size() * sizeof(gf_ptab) + sizeof(gf_ptab)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "rs: matrix");
+  HIPCHK(c, hipMemcpyAsync(c->rs_enc_ptab.p, ptab.data(), ptab.size() * sizeof(gf_ptab), hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->rs_enc.p, M.data(), M.size(), hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->rs_enc_job.p, &job, sizeof(rs_job), hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->rs_enc_coef.p, coef.data(), coef.size() * 2, hipMemcpyHostToDevice, s));
@@ -284,18 +325,22 @@ static int rs_reconstruct(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_presen
                      c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>(), c->rs_jobs_d.as<rs_job>(),
                      c->rs_coef_d.as<uint16_t>(), c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(), d_status);
   HIPCHK(c, hipGetLastError());
-  const dim3 grid((L + 1023) / 1024, inst);
-  {
-    timed t_(c, HBX_K_RS_CODE, s);
-    hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_d.as<rs_job>(),
-                       c->rs_coef_d.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
+  if (L % 4 == 0) {
+    if (!c->rs_ptab_d.ensure((size_t)inst * RS_MAX_N * k * sizeof(gf_ptab)) ||
+        !c->rs_ptab_p.ensure((size_t)inst * RS_MAX_N * k * sizeof(gf_ptab)))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "rs_reconstruct: out of device memory");
+    const dim3 tg((RS_MAX_N * k + 255) / 256, inst);
+    hipLaunchKernelGGL(k_rs_perm_tables, tg, dim3(256), 0, s, c->rs_jobs_d.as<rs_job>(), c->rs_coef_d.as<uint16_t>(), k,
+                       c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>(), c->rs_ptab_d.as<gf_ptab>());
+    hipLaunchKernelGGL(k_rs_perm_tables, tg, dim3(256), 0, s, c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(), k,
+                       c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>(), c->rs_ptab_p.as<gf_ptab>());
+    HIPCHK(c, hipGetLastError());
   }
+  rs_code(c, d_shards, stride, L, k, inst, c->rs_jobs_d.as<rs_job>(), c->rs_coef_d.as<uint16_t>(),
+          c->rs_ptab_d.as<gf_ptab>(), 1u, s);
   HIPCHK(c, hipGetLastError());
-  {
-    timed t_(c, HBX_K_RS_CODE, s);
-    hipLaunchKernelGGL(k_rs_code, grid, dim3(256), 0, s, d_shards, stride, L, k, c->rs_jobs_p.as<rs_job>(),
-                       c->rs_coef_p.as<uint16_t>(), 1u, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
-  }
+  rs_code(c, d_shards, stride, L, k, inst, c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(),
+          c->rs_ptab_p.as<gf_ptab>(), 1u, s);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -351,7 +396,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
-                  &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef,
+                  &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef, &c->rs_enc_ptab, &c->rs_ptab_d, &c->rs_ptab_p,
                   &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots,
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
@@ -373,6 +418,13 @@ int hbx_set_digest(hbx_ctx* c, int variant) {
   c->verified_p = 0;
   c->coin_I = 0;
   c->coin_n = 0;
+  return HBX_OK;
+}
+
+int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
+  if (!c || (lanes != 0 && lanes != 1 && lanes != 3))
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1 or 3, not %d", lanes);
+  c->verify_lanes = lanes;
   return HBX_OK;
 }
 
@@ -556,14 +608,24 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     if (rc) return rc;
     c->ct_known = true;
   }
-  // share checks: throughput-bound, n*p checks -> one lane each
+  // share checks: one lane per check when the launch fills the chip (throughput), else three
+  // lanes per check (latency: an epoch shard on one of several GPUs; pairing3.hpp)
   {
     timed t_(c, HBX_K_VERIFY_SHARES, s);
-    hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
-                       c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
-                       c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
-                       own ? c->own_me : UINT32_MAX,
-                       (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
+    const size_t waves1 = (size_t)((n + 63) / 64) * p;
+    const bool three = c->verify_lanes == 3 || (c->verify_lanes == 0 && waves1 < (size_t)VERIFY_FILL_WAVES);
+    if (three)
+      hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
+                         c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
+                         c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
+                         c->valid.as<uint8_t>(), own ? c->own_me : UINT32_MAX,
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
+    else
+      hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
+                         c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
+                         c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
+                         own ? c->own_me : UINT32_MAX,
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
   }
   HIPCHK(c, hipGetLastError());
   c->ct_known = true;
@@ -608,12 +670,8 @@ int hbx_rs_encode_d(hbx_ctx* c, uint8_t* d_shards, uint32_t inst, uint32_t k, ui
   if (m == 0) return HBX_OK;  // Coding::Trivial
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
-  {
-    timed t_(c, HBX_K_RS_CODE, s);
-    hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, L, k,
-                       c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(), 0u, c->gf_log.as<uint16_t>(),
-                       c->gf_exp.as<uint8_t>());
-  }
+  rs_code(c, d_shards, (size_t)(k + m) * L, L, k, inst, c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(),
+          c->rs_enc_ptab.as<gf_ptab>(), 0u, s);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }

@@ -15,6 +15,7 @@
 #include "../../include/hbx.h"
 #include "hash.hpp"
 #include "pairing.hpp"
+#include "pairing3.hpp"
 #include "wide.hpp"
 
 namespace hbx {
@@ -318,6 +319,37 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   }
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
   if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+}
+
+// k_verify_shares with THREE lanes per share (pairing3.hpp): 21 checks per wave, ~2.5x lower
+// latency per check.  Used when a launch has too few shares to fill the chip one lane per share
+// (an epoch shard on one of several GPUs).  Same inputs, outputs and own-share semantics.
+__global__ void __launch_bounds__(64) k_verify_shares3(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
+                                                       const uint8_t* __restrict__ present,
+                                                       const g1a* __restrict__ pk, uint32_t n_keys,
+                                                       const g2a* __restrict__ G2pts,
+                                                       const line_block* __restrict__ lines,
+                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
+                                                       uint8_t* __restrict__ valid, uint32_t me,
+                                                       uint8_t* __restrict__ ct_valid) {
+  const int lane = (int)(threadIdx.x & 63);
+  const grp3 g = grp3_of_lane();
+  const uint32_t i = blockIdx.x * G3_PER_WAVE + (uint32_t)(lane / G3);
+  const uint32_t j = blockIdx.y;
+  if (lane == 63 || i >= n) return;  // whole groups
+  const size_t idx = (size_t)j * n + i;
+  const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
+                                     ct_ok[j] != 0);
+  bool v = false;
+  if (res == HBX_SHARE_VALID) {
+    g1a npk = pk[i];
+    npk.y = fq_neg(npk.y);
+    v = check2_g3(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf, g);
+  }
+  if (g.gl == 0) {
+    valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+    if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+  }
 }
 
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with

@@ -24,19 +24,6 @@ struct line_pre {
   fq2 c0, c1;
 };
 
-// Load of read-only data at a wave-uniform address through the constant address space, so it
-// is issued as scalar (SMEM) loads through the scalar cache: a plain global load after an
-// out-of-line call cannot be proven unclobbered and would be a vector load per lane.
-template <class T>
-HBX_HD T ld_uniform(const T* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  typedef __attribute__((address_space(4))) const T* cptr;
-  return *(cptr)p;
-#else
-  return *p;
-#endif
-}
-
 // Raw line through the doubling of T (Jacobian), scaled by 2 Y Z^3:
 //   c0 = 3X^3 - 2Y^2, c1 = -3X^2 Z^2, c2 = 2YZ^3;  T <- 2T.
 HBX_HDNI void line_dbl_step(g2j& T, fq2& c0, fq2& c1, fq2& c2) {

@@ -64,6 +64,7 @@ EXPORTS = (
     "hbx_get_ct_hashes",
     "hbx_set_digest",
     "hbx_set_merkle_digest",
+    "hbx_set_verify_lanes",
     "hbx_merkle_node_count",
     "hbx_merkle_build_d",
     "hbx_merkle_proofs_d",
@@ -142,6 +143,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_kernel_time.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
     lib.hbx_set_digest.argtypes = [P, ctypes.c_int]
     lib.hbx_set_merkle_digest.argtypes = [P, ctypes.c_int]
+    lib.hbx_set_verify_lanes.argtypes = [P, ctypes.c_int]
     lib.hbx_merkle_node_count.argtypes = [u32]
     lib.hbx_merkle_node_count.restype = u32
     lib.hbx_merkle_build_d.argtypes = [P, P, u32, u32, u32, P, P, P]
@@ -201,6 +203,10 @@ class Context:
     def set_digest(self, variant: int):
         """hbx_set_digest: DIGEST_SHA256 (default) or DIGEST_SHA3_256 for hash_g2 / hash_g1_g2 / hash_bytes."""
         self._check(self.lib.hbx_set_digest(self.h, variant))
+
+    def set_verify_lanes(self, lanes: int):
+        """hbx_set_verify_lanes: 0 auto (default), 1 or 3 lanes per decryption-share check."""
+        self._check(self.lib.hbx_set_verify_lanes(self.h, lanes))
 
     def set_merkle_digest(self, variant: int):
         """hbx_set_merkle_digest: MERKLE_SHA256 (default, afck merkle) or MERKLE_SHA3."""

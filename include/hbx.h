@@ -132,6 +132,11 @@ int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launch
  * hbx_set_merkle_digest -- the Merkle tree of the broadcast calls (HBX_MERKLE_*).
  * ------------------------------------------------------------------------------------------- */
 int hbx_set_digest(hbx_ctx* ctx, int variant);
+/* Lanes per decryption-share check (no reference counterpart; results identical): 1 = one lane
+ * per check (throughput when a launch has >= 1024 waves of checks), 3 = three cooperating lanes
+ * per check (~2.5x lower latency per check: epoch shards on one of several GPUs), 0 = choose by
+ * launch size (default). */
+int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
 int hbx_set_merkle_digest(hbx_ctx* ctx, int variant);
 
 /* ---------------------------------------------------------------------------------------------

@@ -29,4 +29,5 @@ def _default_digests(request):
         ctx = request.getfixturevalue("hbx_ctx")
         ctx.set_digest(0)
         ctx.set_merkle_digest(0)
+        ctx.set_verify_lanes(0)
     yield

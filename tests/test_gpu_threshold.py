@@ -212,3 +212,24 @@ def test_decrypt_shares_match_oracle(hbx_ctx, name):
     want = d["shares"][keep]
     mask = ~d["corrupt"][keep] & d["present"][keep] & (d["expect_share_status"][keep] != 3)
     np.testing.assert_array_equal(sh[mask], want[mask])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256",
+                                  "hb_epoch_n7_sha3"])
+def test_one_lane_checks_match_golden(hbx_ctx, name):
+    """The fixtures' launches are small, so the default (auto) path above runs the three-lane
+    share check (pairing3.hpp); this forces the one-lane kernel (hbx_set_verify_lanes(1), what a
+    full N = 256 epoch on one GPU uses) through the same expectations, plain and own-share mode."""
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
+    hbx_ctx.set_verify_lanes(1)
+    try:
+        _device_epoch(hbx_ctx, d, own=False)
+        hbx_ctx.set_own_share(int(d["own_me"]), d["own_sk"].tobytes())
+        try:
+            _device_epoch(hbx_ctx, d, own=True)
+        finally:
+            hbx_ctx.set_own_share(0, None)
+    finally:
+        hbx_ctx.set_verify_lanes(0)
