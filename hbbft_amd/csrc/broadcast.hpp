@@ -144,52 +144,102 @@ __global__ void __launch_bounds__(256) k_rs_perm_tables(const rs_job* __restrict
   tables[(size_t)inst * RS_MAX_N * k + e] = t;
 }
 
+// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // out rows = XOR_c coef[o][c] * in rows c, byte columns; needs L % 4 == 0 (dword rows).  A wave
-// covers 64 * D consecutive dwords of every row (lane l: dwords l, l + 64, ...), accumulating CH
-// output rows per pass over the inputs.  grid (ceil(L / (4 * 256 * D)), inst); job_stride as
-// k_rs_code (0: all instances run job 0 with tables[0], 1: per-instance jobs and tables).
+// covers 64 * D consecutive dwords of every row (lane l: dwords l, l + 64, ...) and accumulates
+// CH output rows per pass over the inputs, two inputs per step so the 6 lookups of a step fold
+// into the accumulator with 3 v_bitop3 (4.5 VALU ops per coefficient and data dword).  The
+// pass's tables are staged in LDS ([c][o]: T0/T1 as one 16-byte entry, T2 packed 4 per entry;
+// wave-uniform broadcast reads); outputs past n_out get zero tables and are not stored, inputs
+// are read one step ahead of use.  grid (ceil(L / (4 * 256 * D)), inst), dynamic LDS
+// rs_perm_lds_bytes(k, CH); job_stride as k_rs_code (0: job 0 / tables[0] for all instances).
+__host__ __device__ constexpr size_t rs_perm_lds_bytes(uint32_t k, int ch) {
+  return (size_t)((k + 1) & ~1u) * ch * 20;
+}
+
 template <int CH, int D>
 __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
                                                       uint32_t k, const rs_job* __restrict__ jobs,
                                                       const gf_ptab* __restrict__ tables, uint32_t job_stride) {
+  static_assert(CH % 4 == 0, "T2 entries are packed four per 16 bytes");
+  extern __shared__ uint4 rs_lds[];
+  const uint32_t kp = (k + 1) & ~1u;
+  uint4* tab01 = rs_lds;                 // [kp][CH]
+  uint4* tab2 = rs_lds + (size_t)kp * CH;  // [kp][CH / 4]
   const uint32_t inst = blockIdx.y;
   const rs_job* J = jobs + (size_t)inst * job_stride;
   const int no = ld_uniform(&J->n_out);
+  if (no == 0) return;
   const uint32_t Ld = L >> 2;
-  const uint32_t wave0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * D;
-  if (no == 0 || wave0 >= Ld) return;
   const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * D;
   uint32_t* base = reinterpret_cast<uint32_t*>(shards + (size_t)inst * inst_stride);
   const gf_ptab* tb = tables + (size_t)inst * job_stride * RS_MAX_N * k;
   bool ok[D];
 #pragma unroll
   for (int j = 0; j < D; j++) ok[j] = wave0 + lane + 64 * j < Ld;
+  auto load_in = [&](uint32_t c, uint32_t* d) {
+    if (c < k) {
+      const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c]) * Ld + wave0 + lane;
+#pragma unroll
+      for (int j = 0; j < D; j++) d[j] = ok[j] ? src[64 * j] : 0u;
+    } else {
+#pragma unroll
+      for (int j = 0; j < D; j++) d[j] = 0u;
+    }
+  };
   for (int o0 = 0; o0 < no; o0 += CH) {
+    __syncthreads();  // previous pass done with the tables
+    for (uint32_t e = threadIdx.x; e < kp * CH; e += blockDim.x) {
+      const uint32_t c = e / CH, o = e % CH;
+      gf_ptab t{};
+      if (c < k && o0 + (int)o < no) t = tb[(size_t)(o0 + o) * k + c];
+      tab01[e] = make_uint4(t.w[0], t.w[1], t.w[2], t.w[3]);
+      reinterpret_cast<uint32_t*>(tab2)[e] = t.w[4];
+    }
+    __syncthreads();
     uint32_t acc[CH][D];
 #pragma unroll
     for (int o = 0; o < CH; o++)
 #pragma unroll
       for (int j = 0; j < D; j++) acc[o][j] = 0;
+    uint32_t na[D], nb[D];
+    load_in(0, na);
+    load_in(1, nb);
 #pragma unroll 1
-    for (uint32_t c = 0; c < k; c++) {
-      const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c]) * Ld + wave0 + lane;
-      uint32_t s0[D], s1[D], s2[D];
+    for (uint32_t c = 0; c < kp; c += 2) {
+      uint32_t a0[D], a1[D], a2[D], b0[D], b1[D], b2[D];
 #pragma unroll
       for (int j = 0; j < D; j++) {
-        const uint32_t d = ok[j] ? src[64 * j] : 0u;
-        s0[j] = d & 0x07070707u;
-        s1[j] = (d >> 3) & 0x07070707u;
-        s2[j] = (d >> 6) & 0x03030303u;
+        a0[j] = na[j] & 0x07070707u;
+        a1[j] = (na[j] >> 3) & 0x07070707u;
+        a2[j] = (na[j] >> 6) & 0x03030303u;
+        b0[j] = nb[j] & 0x07070707u;
+        b1[j] = (nb[j] >> 3) & 0x07070707u;
+        b2[j] = (nb[j] >> 6) & 0x03030303u;
       }
-      const gf_ptab* t = tb + c;
+      load_in(c + 2, na);
+      load_in(c + 3, nb);
+      const uint4* ta = tab01 + (size_t)c * CH;
+      const uint4* tc = tab2 + (size_t)c * (CH / 4);
 #pragma unroll
-      for (int o = 0; o < CH; o++) {
-        if (o0 + o < no) {
-          const gf_ptab T = ld_uniform(t + (size_t)(o0 + o) * k);
+      for (int o4 = 0; o4 < CH; o4 += 4) {
+        const uint4 t2a = tc[o4 / 4], t2b = tc[CH / 4 + o4 / 4];
+        const uint32_t t2av[4] = {t2a.x, t2a.y, t2a.z, t2a.w}, t2bv[4] = {t2b.x, t2b.y, t2b.z, t2b.w};
 #pragma unroll
-          for (int j = 0; j < D; j++)
-            acc[o][j] ^= __builtin_amdgcn_perm(T.w[1], T.w[0], s0[j]) ^ __builtin_amdgcn_perm(T.w[3], T.w[2], s1[j]) ^
-                         __builtin_amdgcn_perm(0u, T.w[4], s2[j]);
+        for (int q = 0; q < 4; q++) {
+          const int o = o4 + q;
+          const uint4 A = ta[o], B = ta[CH + o];
+#pragma unroll
+          for (int j = 0; j < D; j++) {
+            uint32_t x = xor3(acc[o][j], __builtin_amdgcn_perm(A.y, A.x, a0[j]), __builtin_amdgcn_perm(A.w, A.z, a1[j]));
+            x = xor3(x, __builtin_amdgcn_perm(0u, t2av[q], a2[j]), __builtin_amdgcn_perm(B.y, B.x, b0[j]));
+            acc[o][j] = xor3(x, __builtin_amdgcn_perm(B.w, B.z, b1[j]), __builtin_amdgcn_perm(0u, t2bv[q], b2[j]));
+          }
         }
       }
     }
@@ -492,6 +542,122 @@ __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict_
   for (int q = 0; q < 8; q++) o[q] = h[q];
 }
 
+// SHA-256 Merkle leaves (HBX_MERKLE_SHA256), two waves per 64 leaves of one instance:
+//  * wave 1 (producer) loads each leaf's next 64-byte block, expands the message schedule and
+//    writes K[t] + W[t] for t < 64 to LDS, one block ahead of the consumer, with the raw words of
+//    the block after that already in flight (register prefetch);
+//  * wave 0 (consumer) runs only the 64 rounds from LDS: the serial chain of a leaf -- the
+//    bound of this kernel, since a C5 epoch has just n x inst = 16,384 independent leaves of 373
+//    blocks each -- carries no global loads, no schedule and no scratch round trips.
+// Same digests as k_merkle_leaves (leaf = SHA-256(0x00 || i || shard_i)).
+// grid (ceil(n / 64), inst), 128 threads.
+__device__ __forceinline__ uint32_t sha_sig(uint32_t x, int r1, int r2, int r3) {
+  return xor3(rotr32(x, r1), rotr32(x, r2), rotr32(x, r3));
+}
+
+__global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __restrict__ shards, size_t inst_stride,
+                                                              uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash) {
+  __shared__ uint4 kw[2][16][64];  // [slot][rounds / 4][lane]
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * 64 + lane, inst = blockIdx.y;
+  const bool live = i < n;
+  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)(live ? i : 0) * L;
+  const uint32_t prefix = (i & 0xFF) << 8;  // bytes 0x00, i
+  const uint64_t total = 2 + (uint64_t)L;
+  const uint64_t nblocks = (total + 9 + 63) / 64;
+  // producer state: raw dwords of the next block (fast blocks: whole 64 bytes of shard data)
+  uint32_t raw[17];
+  auto fast = [&](uint64_t b) { return b * 64 >= 2 && b * 64 + 64 <= total; };
+  auto fetch = [&](uint64_t b) {
+    if (b < nblocks && fast(b)) {
+      const uint8_t* q = data + (b * 64 - 2);
+      const uint32_t* pa = reinterpret_cast<const uint32_t*>((uintptr_t)q & ~(uintptr_t)3);
+#pragma unroll
+      for (int k = 0; k < 16; k++) raw[k] = pa[k];
+      // a misaligned block needs a 17th dword (it holds block bytes, so it is inside the buffer)
+      raw[16] = ((uintptr_t)q & 3) ? pa[16] : 0u;
+    }
+  };
+  auto produce = [&](uint64_t b, int slot) {
+    uint32_t w[16];
+    if (fast(b)) {
+      const uint32_t sh = (uint32_t)(((uintptr_t)data + b * 64 - 2) & 3);
+#pragma unroll
+      for (int k = 0; k < 16; k++) w[k] = bswap32(__builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh));
+    } else {
+      const uint64_t b0 = b * 64;
+#pragma unroll 1
+      for (int k = 0; k < 16; k++) {
+        uint32_t word = 0;
+        for (int q = 0; q < 4; q++) {
+          const uint64_t pos = b0 + 4 * k + q;
+          uint8_t byte;
+          if (pos < total) byte = msg_byte(prefix, 2, data, L, pos);
+          else if (pos == total) byte = 0x80;
+          else if (pos >= nblocks * 64 - 8) byte = (uint8_t)((total * 8) >> (8 * (nblocks * 64 - 1 - pos)));
+          else byte = 0;
+          word = (word << 8) | byte;
+        }
+        w[k] = word;
+      }
+    }
+    fetch(b + 1);  // next block's raw words load while this schedule is expanded
+#pragma unroll
+    for (int t4 = 0; t4 < 16; t4++) {
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int t = 4 * t4 + q;
+        uint32_t wt;
+        if (t < 16) {
+          wt = w[t];
+        } else {
+          const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+          const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+          const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+          wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+          w[t & 15] = wt;
+        }
+        o[q] = wt + SHA256_K[t];
+      }
+      kw[slot][t4][lane] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  };
+  uint32_t H[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  if (wave == 1) {
+    fetch(0);
+    produce(0, 0);
+  }
+  __syncthreads();
+  for (uint64_t b = 0; b < nblocks; b++) {
+    const int slot = (int)(b & 1);
+    if (wave == 0) {
+      uint32_t a = H[0], bb = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+      for (int t4 = 0; t4 < 16; t4++) {
+        const uint4 k4 = kw[slot][t4][lane];
+        const uint32_t kv[4] = {k4.x, k4.y, k4.z, k4.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t t1 = h + sha_sig(e, 6, 11, 25) + ((e & f) ^ (~e & g)) + kv[q];
+          const uint32_t t2 = sha_sig(a, 2, 13, 22) + ((a & bb) ^ (a & c) ^ (bb & c));
+          h = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + t2;
+        }
+      }
+      H[0] += a; H[1] += bb; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+    } else if (b + 1 < nblocks) {
+      produce(b + 1, slot ^ 1);
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && live) {
+    uint32_t* o = leaf_hash + ((size_t)inst * n + i) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; q++) o[q] = H[q];
+  }
+}
+
 // Number of stored tree nodes for n leaves: every level from the leaves (n) to the root (1),
 // with a promoted odd node stored again on the level it moves to.
 __host__ __device__ inline uint32_t merkle_node_count(uint32_t n) {
@@ -664,21 +830,23 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
   valid[j] = ok ? 1 : 0;
 }
 
-// glue_shards (broadcast.rs:697-707) of instances whose root matched: value = the first k
-// shards concatenated, BE u32 length, then that many bytes (fewer if the data runs out).
-// One block per instance.  status in/out: 0 ok (-> HBX_E_NO_PAYLOAD if fewer than 4 bytes).
+// glue_shards (broadcast.rs:697-707): the payload is bytes [4, 4 + len) of the first k shards
+// (contiguous), len = the big-endian u32 header clamped to the available bytes.  grid
+// (ceil(max_len / 4096), inst): thread = 16 output bytes, dword loads/stores when source and
+// destination rows are dword-aligned (byte copy otherwise).
 __global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards, size_t inst_stride, uint32_t k,
                                               uint32_t L, uint8_t* __restrict__ out, size_t out_stride,
                                               uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
-  const uint32_t inst = blockIdx.x;
+  const uint32_t inst = blockIdx.y;
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
   if (status[inst] != 0) {
-    if (threadIdx.x == 0) out_len[inst] = 0;
+    if (lead) out_len[inst] = 0;
     return;
   }
   const uint8_t* base = shards + (size_t)inst * inst_stride;  // shards 0..k-1 are contiguous
   const uint64_t total = (uint64_t)k * L;
   if (total < 4) {
-    if (threadIdx.x == 0) {
+    if (lead) {  // the other blocks of the instance return here or above either way
       status[inst] = -11;
       out_len[inst] = 0;
     }
@@ -686,8 +854,23 @@ __global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards
   }
   const uint64_t want = ((uint64_t)base[0] << 24) | ((uint64_t)base[1] << 16) | ((uint64_t)base[2] << 8) | base[3];
   const uint64_t len = want < total - 4 ? want : total - 4;
-  for (uint64_t q = threadIdx.x; q < len; q += blockDim.x) out[(size_t)inst * out_stride + q] = base[4 + q];
-  if (threadIdx.x == 0) out_len[inst] = len;
+  if (lead) out_len[inst] = len;
+  const uint64_t q0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (q0 >= len) return;
+  const uint8_t* src = base + 4 + q0;
+  uint8_t* dst = out + (size_t)inst * out_stride + q0;
+  if (q0 + 16 <= len && (((uintptr_t)src | (uintptr_t)dst) & 3) == 0) {
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+    const uint32_t v0 = s4[0], v1 = s4[1], v2 = s4[2], v3 = s4[3];
+    d4[0] = v0;
+    d4[1] = v1;
+    d4[2] = v2;
+    d4[3] = v3;
+  } else {
+    const uint64_t end = q0 + 16 < len ? 16 : len - q0;
+    for (uint64_t q = 0; q < end; q++) dst[q] = src[q];
+  }
 }
 
 // status = root(inst) == expected ? status : HBX_E_ROOT_MISMATCH

@@ -6,6 +6,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -228,15 +229,38 @@ static gf_ptab gf_perm_table(uint8_t c) {
   return t;
 }
 
+// Output rows x dwords per lane of the byte-permute kernel; HBX_RS_TILE (0..4) selects one of
+// the compiled variants for tuning.
+static int rs_tile() {
+  static const int t = [] {
+    const char* e = getenv("HBX_RS_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  return t;
+}
+
 // One coding pass: the byte-permute kernel when rows are whole dwords, else the LDS log/exp one.
 static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, uint32_t k, uint32_t inst,
                     const rs_job* jobs, const uint16_t* coef, const gf_ptab* ptab, uint32_t job_stride, hipStream_t s) {
   timed t_(c, HBX_K_RS_CODE, s);
   if (L % 4 == 0) {
-    constexpr int CH = 48, D = 2;
     const uint32_t Ld = L / 4;
-    const dim3 grid((Ld + 256 * D - 1) / (256 * D), inst);
-    hipLaunchKernelGGL((k_rs_code_perm<CH, D>), grid, dim3(256), 0, s, d_shards, stride, L, k, jobs, ptab, job_stride);
+    static const int tile_ch[] = {32, 32, 64, 24, 48};
+    int tile = rs_tile();
+    if (tile < 0 || tile > 4) tile = 0;
+    if (rs_perm_lds_bytes(k, tile_ch[tile]) > 65536) tile = 3;  // 24 x 128 x 20 B fits any k
+    switch (tile) {
+#define HBX_RS_TILE(ch, d)                                                                                        \
+  hipLaunchKernelGGL((k_rs_code_perm<ch, d>), dim3((Ld + 256 * d - 1) / (256 * d), inst), dim3(256),               \
+                     rs_perm_lds_bytes(k, ch), s, d_shards, stride, L, k, jobs, ptab, job_stride);                 \
+  break;
+      case 1: HBX_RS_TILE(32, 4)
+      case 2: HBX_RS_TILE(64, 2)
+      case 3: HBX_RS_TILE(24, 4)
+      case 4: HBX_RS_TILE(48, 2)
+      default: HBX_RS_TILE(32, 2)
+#undef HBX_RS_TILE
+    }
   } else {
     hipLaunchKernelGGL(k_rs_code, dim3((L + 1023) / 1024, inst), dim3(256), 0, s, d_shards, stride, L, k, jobs, coef,
                        job_stride, c->gf_log.as<uint16_t>(), c->gf_exp.as<uint8_t>());
@@ -351,8 +375,12 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
   if (!c->leaf_hash.ensure((size_t)inst * n * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: leaf hashes");
   {
     timed t_(c, HBX_K_MERKLE_LEAVES, s);
-    hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                       c->leaf_hash.as<uint32_t>(), c->merkle);
+    if (c->merkle == HBX_MERKLE_SHA256)
+      hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((n + 63) / 64, inst), dim3(128), 0, s, d_shards, (size_t)n * L,
+                         n, L, c->leaf_hash.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
+                         c->leaf_hash.as<uint32_t>(), c->merkle);
   }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots, d_nodes,
@@ -753,7 +781,8 @@ int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_prese
   hipLaunchKernelGGL(k_root_check, dim3((inst + 63) / 64), dim3(64), 0, s, c->roots.as<uint8_t>(), d_root_expect, inst,
                      d_status);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_glue, dim3(inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, k, L, d_out,
+  const uint64_t glue_blocks = ((uint64_t)k * L + 4095) / 4096;
+  hipLaunchKernelGGL(k_glue, dim3((unsigned)glue_blocks, inst), dim3(256), 0, s, d_shards, (size_t)(k + m) * L, k, L, d_out,
                      (size_t)out_stride, d_out_len, d_status);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
