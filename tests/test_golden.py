@@ -91,3 +91,27 @@ def test_coin_fixture_against_oracle(n):
     h0 = bls.g2_decompress(d["h"][0].tobytes())
     assert tc.verify_sig(bls.g1_decompress(d["master_pk"].tobytes()), sig, nonces[0], hash_pt=h0)
     assert tc.parity(sig) == bool(d["expect_parity"][0])
+
+
+def test_c5_fixture_against_oracle():
+    """tests/golden/c5_broadcast.npz (BASELINE config C5) is what oracle/rs_merkle.py gives for
+    the seeded 1 MiB proposal: shard digests, both Merkle roots, the proof lemmas."""
+    import hashlib
+
+    from oracle import rs_merkle as rm
+
+    g = np.load(os.path.join(GOLDEN, "c5_broadcast.npz"))
+    n, plen = int(g["n"]), int(g["plen"])
+    value = np.random.default_rng(int(g["seed"])).integers(0, 256, size=plen, dtype=np.uint8).tobytes()
+    assert hashlib.sha256(value).digest() == g["payload_sha"].tobytes()
+    shards, leaves, tree = rm.send_shards(value, n)
+    assert shards.shape == (n, int(g["shard_len"]))
+    for i in range(n):
+        assert hashlib.sha256(shards[i].tobytes()).digest() == g["shard_sha"][i].tobytes()
+    assert tree.root_hash() == g["root_sha256"].tobytes()
+    assert rm.MerkleTree(leaves, "sha3").root_hash() == g["root_sha3"].tobytes()
+    for j, leaf in enumerate(g["proof_leaves"]):
+        p = tree.gen_proof(leaves[int(leaf)])
+        assert len(p["lemma"]) - 1 == int(g["proof_depth"][j])
+        for lv, (h, _sib) in enumerate(p["lemma"]):
+            assert h == g["proof_nodes"][j, lv].tobytes()

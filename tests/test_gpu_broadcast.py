@@ -275,3 +275,64 @@ def test_merkle_sha3_validate_and_decode(hbx_ctx, n):
     st = st.cpu().numpy()
     assert st[0] == 0 and out[0, : int(out_len[0])].cpu().numpy().tobytes() == value
     assert st[1] == HBX_E_ROOT_MISMATCH
+
+
+# ---- BASELINE config C5: one 1 MiB proposal at N=128 against the committed
+# fixture tests/golden/c5_broadcast.npz (tests/golden/make_c5_golden.py) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["sha256", "sha3"])
+def test_c5_fixture(hbx_ctx, variant):
+    import hashlib
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c5_broadcast.npz"))
+    n, k, m, L, plen = int(g["n"]), int(g["k"]), int(g["m"]), int(g["shard_len"]), int(g["plen"])
+    value = np.random.default_rng(int(g["seed"])).integers(0, 256, size=plen, dtype=np.uint8).tobytes()
+    assert hashlib.sha256(value).digest() == g["payload_sha"].tobytes()
+    _set_merkle(hbx_ctx, variant)
+    # send_shards: frame, RS encode (broadcast.rs:341-367)
+    framed = int(plen).to_bytes(4, "big") + value
+    buf = np.zeros((1, n, L), dtype=np.uint8)
+    buf.reshape(-1)[: len(framed)] = np.frombuffer(framed, dtype=np.uint8)
+    d = dev(buf)
+    hbx_ctx.rs_encode_d(d, k, m)
+    torch.cuda.synchronize()
+    shards = d.cpu().numpy()[0]
+    got = np.stack([np.frombuffer(hashlib.sha256(shards[i].tobytes()).digest(), dtype=np.uint8) for i in range(n)])
+    np.testing.assert_array_equal(got, g["shard_sha"])
+    # Merkle tree (broadcast.rs:381): every node, root, and the proofs of the fixture's leaves
+    cnt = hbx_ctx.merkle_node_count(n)
+    assert cnt == int(g[f"node_count_{variant}"])
+    nodes = torch.zeros((1, cnt, 32), dtype=torch.uint8, device="cuda")
+    roots = torch.zeros((1, 32), dtype=torch.uint8, device="cuda")
+    hbx_ctx.merkle_build_d(d, nodes, roots)
+    torch.cuda.synchronize()
+    assert roots.cpu().numpy()[0].tobytes() == g[f"root_{variant}"].tobytes()
+    assert hashlib.sha256(nodes.cpu().numpy().tobytes()).digest() == g[f"nodes_sha_{variant}"].tobytes()
+    if variant == "sha256":
+        req = np.array([(0, j) for j in g["proof_leaves"]], dtype=np.uint32)
+        P = len(req)
+        nh = torch.zeros((P, 17, 32), dtype=torch.uint8, device="cuda")
+        sh = torch.zeros((P, 16, 32), dtype=torch.uint8, device="cuda")
+        sides = torch.zeros(P, dtype=torch.int32, device="cuda")
+        depth = torch.zeros(P, dtype=torch.int32, device="cuda")
+        proot = torch.zeros((P, 32), dtype=torch.uint8, device="cuda")
+        hbx_ctx.merkle_proofs_d(nodes, n, dev(req), nh, sh, sides, depth, proot)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(depth.cpu().numpy(), g["proof_depth"])
+        np.testing.assert_array_equal(sides.cpu().numpy(), g["proof_sides"])
+        np.testing.assert_array_equal(nh.cpu().numpy(), g["proof_nodes"])
+        np.testing.assert_array_equal(sh.cpu().numpy(), g["proof_sibs"])
+    # decode_from_shards with the last f shards missing (broadcast.rs:660-707)
+    f = (n - 1) // 3
+    present = np.ones((1, n), dtype=np.uint8)
+    present[0, n - f:] = 0
+    work = shards[None].copy()
+    work[present == 0] = 0xA5
+    out = torch.zeros((1, k * L), dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    hbx_ctx.broadcast_decode_d(dev(work), dev(present), dev(g[f"root_{variant}"][None].copy()), k, m, out, out_len, st)
+    torch.cuda.synchronize()
+    assert int(st.cpu()[0]) == 0 and int(out_len.cpu()[0]) == plen
+    assert hashlib.sha256(out.cpu().numpy()[0, :plen].tobytes()).digest() == g["payload_sha"].tobytes()
