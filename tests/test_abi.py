@@ -50,7 +50,9 @@ def test_shard_layout():
     from hbbft_amd import shard
 
     assert shard.proposer_range(256, 8, 3) == (96, 128)
+    # N % G != 0: balanced contiguous ranges covering every proposer once
+    assert [shard.proposer_range(10, 4, r) for r in range(4)] == [(0, 3), (3, 6), (6, 8), (8, 10)]
     with pytest.raises(ValueError):
-        shard.proposer_range(10, 4, 0)
+        shard.proposer_range(10, 4, 4)
     lay = shard.slab_layout(256, 32)
     assert lay["size"] == 256 * 32 + 32 + 128
