@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--no-own-share", action="store_true",
                     help="run Ciphertext::verify as separate checks instead of through the node's own share")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 3),
+                    help="lanes per decryption-share check (0: auto by occupancy)")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
@@ -230,6 +232,7 @@ def main():
         lo, hi = 0, n
     pj = hi - lo
     ctx = Context(local)
+    ctx.set_verify_lanes(args.verify_lanes)
     ep = make_epoch(ctx, n, lo, hi, args.vlen, args.corrupt_every)
     st = ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]])
     assert (st == 0).all()

@@ -314,6 +314,53 @@ HBX_HDNI g2j g2_add(const g2j& p, const g2j& q) {
 
 HBX_HD g2j g2_neg(const g2j& p) { return g2j{p.x, fq2_neg(p.y), p.z}; }
 
+// p + q for an affine q (Z2 = 1): 7M + 4S instead of 12M + 4S.
+HBX_HDNI g2j g2_add_mixed(const g2j& p, const g2a& q) {
+  if (q.inf) return p;
+  if (g2j_is_identity(p)) return g2j{q.x, q.y, fq2_one()};
+  const fq2 Z1Z1 = fq2_sqr(p.z);
+  const fq2 U2 = fq2_mul(q.x, Z1Z1);
+  const fq2 S2 = fq2_mul(fq2_mul(q.y, p.z), Z1Z1);
+  if (fq2_eq(p.x, U2)) {
+    if (fq2_eq(p.y, S2)) return g2_dbl(p);
+    return g2_identity();
+  }
+  const fq2 H = fq2_sub(U2, p.x);
+  const fq2 HH = fq2_sqr(H);
+  const fq2 I = fq2_dbl(fq2_dbl(HH));
+  const fq2 J = fq2_mul(H, I);
+  const fq2 r = fq2_dbl(fq2_sub(S2, p.y));
+  const fq2 V = fq2_mul(p.x, I);
+  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr(r), J), fq2_dbl(V));
+  const fq2 Y3 = fq2_sub(fq2_mul(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul(p.y, J)));
+  const fq2 Z3 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.z, H)), Z1Z1), HH);
+  return g2j{X3, Y3, Z3};
+}
+
+// k P for a 64-bit k and an affine P, left to right over the non-adjacent form of k (65 digits,
+// about a third nonzero; the negation of an affine point is free).  One addition site per digit
+// with the point selected by sign, so lanes with different scalars share it.
+HBX_HDNI g2j g2_mul_u64_naf(const g2a& P, uint64_t k) {
+  // NAF(k): c = 3k (66 bits as hi:lo), np = c ^ k; digit i is +1 where bit i+1 of np & c is
+  // set, -1 where bit i+1 of np & k is set
+  const uint64_t lo = k + (k << 1);
+  const uint64_t hi = (k >> 63) + (lo < k ? 1u : 0u);  // carry of k + 2k into bit 64
+  const uint64_t np_lo = lo ^ k, np_hi = hi;           // k has no bits >= 64
+  const uint64_t pos_lo = np_lo & lo, pos_hi = np_hi & hi;
+  const uint64_t neg_lo = np_lo & k;
+  g2a negP = P;
+  negP.y = fq2_neg(P.y);
+  g2j acc = g2_identity();
+  for (int i = 65; i >= 0; i--) {  // bit i+1 of the masks <-> digit i
+    const int b = i + 1;
+    const bool pos = b >= 64 ? ((pos_hi >> (b - 64)) & 1) != 0 : ((pos_lo >> b) & 1) != 0;
+    const bool neg = b >= 64 ? false : ((neg_lo >> b) & 1) != 0;
+    if (!g2j_is_identity(acc)) acc = g2_dbl(acc);
+    if (pos || neg) acc = g2_add_mixed(acc, neg ? negP : P);
+  }
+  return acc;
+}
+
 HBX_HDNI g2a g2_to_affine(const g2j& p) {
   g2a r;
   if (g2j_is_identity(p)) {

@@ -110,7 +110,16 @@ HBX_HD void fq_unpack28(const fq& a, uint32_t* d) {
     d[j] = j == 13 ? v : (v & 0x0FFFFFFFu);
   }
 }
-#if defined(__HIP_DEVICE_COMPILE__)
+// Independent accumulator chains per column of the digit product (a*b terms, m*p terms).
+#ifndef HBX_FQ_NA
+#define HBX_FQ_NA 3
+#endif
+#ifndef HBX_FQ_NP
+#define HBX_FQ_NP 2
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBX_FQ_INLINE)
+#define HBX_FQMUL_ATTR __device__ __forceinline__
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define HBX_FQMUL_ATTR __device__ __noinline__
 #else
 #define HBX_FQMUL_ATTR inline
@@ -132,18 +141,24 @@ HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
   for (int k = 0; k < 27; k++) {
     const int jlo = k < 14 ? 0 : k - 13;
     const int jhi = k < 14 ? k : 13;
-    // two interleaved a*b chains and one m*p chain; m_{k-1} p_1 (the only term that waits on
+    // HBX_FQ_NA interleaved a*b chains and HBX_FQ_NP m*p chains (independent accumulators, so
+    // one wave keeps several v_mad_u64_u32 in flight); m_{k-1} p_1 (the only term that waits on
     // the previous digit) is added last
-    uint64_t s0 = acc, s1 = 0, t = 0;
+    uint64_t s[HBX_FQ_NA], t[HBX_FQ_NP];
 #pragma unroll
-    for (int j = jlo; j <= jhi; j++) {
-      if (j & 1) s1 = (uint64_t)A[j] * B[k - j] + s1;
-      else s0 = (uint64_t)A[j] * B[k - j] + s0;
-    }
+    for (int q = 0; q < HBX_FQ_NA; q++) s[q] = q == 0 ? acc : 0;
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NP; q++) t[q] = 0;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++) s[j % HBX_FQ_NA] = (uint64_t)A[j] * B[k - j] + s[j % HBX_FQ_NA];
 #pragma unroll
     for (int j = jlo; j <= jhi; j++)
-      if (j < k - 1) t = (uint64_t)m[j] * FQ_P28[k - j] + t;
-    acc = s0 + s1 + t;
+      if (j < k - 1) t[j % HBX_FQ_NP] = (uint64_t)m[j] * FQ_P28[k - j] + t[j % HBX_FQ_NP];
+    acc = 0;
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NA; q++) acc += s[q];
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NP; q++) acc += t[q];
     if (k >= 1 && k <= 14) acc = (uint64_t)m[k - 1] * FQ_P28[1] + acc;
     if (k < 13) {
       m[k] = ((uint32_t)acc * FQ_INV28) & 0x0FFFFFFFu;
@@ -191,15 +206,23 @@ HBX_FQMUL_ATTR fq fq_sqr_limbs(HBX_P12(a)) {
   for (int k = 0; k < 27; k++) {
     const int jlo = k < 14 ? 0 : k - 13;
     const int jhi = k < 14 ? k : 13;
-    uint64_t s0 = acc, t = 0;
+    uint64_t s[HBX_FQ_NA], t[HBX_FQ_NP];
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NA; q++) s[q] = q == 0 ? acc : 0;
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NP; q++) t[q] = 0;
 #pragma unroll
     for (int j = jlo; j <= jhi; j++)
-      if (j < k - j) s0 = (uint64_t)A2[j] * A[k - j] + s0;
-    if ((k & 1) == 0 && k / 2 <= 13) s0 = (uint64_t)A[k / 2] * A[k / 2] + s0;
+      if (j < k - j) s[j % HBX_FQ_NA] = (uint64_t)A2[j] * A[k - j] + s[j % HBX_FQ_NA];
+    if ((k & 1) == 0 && k / 2 <= 13) s[(k / 2) % HBX_FQ_NA] = (uint64_t)A[k / 2] * A[k / 2] + s[(k / 2) % HBX_FQ_NA];
 #pragma unroll
     for (int j = jlo; j <= jhi; j++)
-      if (j < k - 1) t = (uint64_t)m[j] * FQ_P28[k - j] + t;
-    acc = s0 + t;
+      if (j < k - 1) t[j % HBX_FQ_NP] = (uint64_t)m[j] * FQ_P28[k - j] + t[j % HBX_FQ_NP];
+    acc = 0;
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NA; q++) acc += s[q];
+#pragma unroll
+    for (int q = 0; q < HBX_FQ_NP; q++) acc += t[q];
     if (k >= 1 && k <= 14) acc = (uint64_t)m[k - 1] * FQ_P28[1] + acc;
     if (k < 13) {
       m[k] = ((uint32_t)acc * FQ_INV28) & 0x0FFFFFFFu;

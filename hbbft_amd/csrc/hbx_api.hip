@@ -86,7 +86,8 @@ struct hbx_ctx {
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
-      coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
+      coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96,
+      coin_comb_lines, coin_comb_c2;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
@@ -429,7 +430,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
+                  &c->coin_out96, &c->coin_comb_lines, &c->coin_comb_c2, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -541,12 +542,21 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
     timed t_(c, HBX_K_PREPARE_CT, s);
     const uint32_t hash_blocks = (uint32_t)(((size_t)p * HASH_K + 63) / 64);
     const bool own = c->own_me != UINT32_MAX;
-    const uint32_t dec_blocks = ((own ? 4 : 2) * p + 63) / 64;
+    const uint32_t dec_blocks = (own ? 4 : 2) * ((p + 63) / 64);  // wave-aligned parts (k_prepare_ct)
     if (own && (!c->own_S.ensure((size_t)p * sizeof(g1a)) || !c->own_part.ensure((size_t)2 * p * sizeof(g1j))))
       return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
-    hipLaunchKernelGGL(k_prepare_ct, dim3(hash_blocks + dec_blocks), b64, 0, s, d_u_comp, d_v_blob, d_v_off,
-                       d_w_comp, p, hash_blocks, c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
-                       own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->digest);
+    // HBX_SPLIT_PREP=1 (profiling): the hash part and the decode part as two launches, so a
+    // kernel trace times each chain on its own
+    static const bool split = getenv("HBX_SPLIT_PREP") != nullptr;
+    const uint32_t parts = split ? 2 : 1;
+    for (uint32_t q = 0; q < parts; q++) {
+      const uint32_t b0 = split && q == 1 ? hash_blocks : 0;
+      const uint32_t nb = split ? (q == 0 ? hash_blocks : dec_blocks) : hash_blocks + dec_blocks;
+      hipLaunchKernelGGL(k_prepare_ct, dim3(nb), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, hash_blocks,
+                         c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
+                         own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->digest,
+                         b0);
+    }
     c->own_ready = own;
   }
   HIPCHK(c, hipGetLastError());
@@ -896,7 +906,9 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   const uint32_t I = c->coin_I;
   if (!c->coin_comb.ensure((size_t)I * sizeof(g2a)) || !c->coin_comb_st.ensure((size_t)I * 4) ||
       !c->coin_mpk_comp.ensure(48) || !c->coin_mpk.ensure(sizeof(g1a)) || !c->coin_mpk_st.ensure(4) ||
-      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96))
+      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96) ||
+      !c->coin_comb_lines.ensure((size_t)I * MILLER_LINES * sizeof(line_pre)) ||
+      !c->coin_comb_c2.ensure((size_t)I * MILLER_LINES * sizeof(fq2)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_signatures: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, s, c->coin_mpk_comp.as<uint8_t>(), 1u, c->coin_mpk.as<g1a>(),
@@ -912,9 +924,26 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
                        c->coin_sig.as<g2a>(), c->coin_n, t, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>());
   }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_master_verify, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                     c->coin_H.as<g2a>(), c->coin_mpk.as<g1a>(), c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(),
-                     I, c->coin_ok.as<uint8_t>(), c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
+  // lines of the combined signatures (16-lane groups, then one lane per line for the
+  // normalisation), the master checks three lanes each, parity and encoding
+  {
+    timed t_(c, HBX_K_MASTER_VERIFY, s);
+    hipLaunchKernelGGL(k_prepare_lines, dim3((I * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(), I,
+                       c->coin_comb_lines.as<line_pre>(), c->coin_comb_c2.as<fq2>(), nullptr, 0u, nullptr, nullptr,
+                       nullptr);
+    HIPCHK(c, hipGetLastError());
+    const uint32_t nl = I * MILLER_LINES;
+    hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_comb_lines.as<line_pre>(),
+                       c->coin_comb_c2.as<fq2>(), nl);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_master_verify3, dim3((I + G3_PER_WAVE - 1) / G3_PER_WAVE), dim3(64), 0, s,
+                       c->coin_lines.as<line_pre>(), c->coin_H.as<g2a>(), c->coin_mpk.as<g1a>(),
+                       c->coin_comb_lines.as<line_pre>(), c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), I,
+                       c->coin_ok.as<uint8_t>());
+    HIPCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_sig_parity, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(),
+                     c->coin_comb_st.as<int32_t>(), I, c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
   HIPCHK(c, hipGetLastError());
   std::vector<uint8_t> ok(I), par(I);
   std::vector<int32_t> st(I);

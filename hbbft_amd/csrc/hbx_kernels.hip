@@ -84,22 +84,27 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
                                                    g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
                                                    const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part,
-                                                   int digest) {
-  if (blockIdx.x >= hash_blocks) {
-    // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2)
-    const uint32_t k = (blockIdx.x - hash_blocks) * blockDim.x + threadIdx.x;
+                                                   int digest, uint32_t block0) {
+  const uint32_t bid = blockIdx.x + block0;  // block0 > 0: the decode part launched on its own
+  if (bid >= hash_blocks) {
+    // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2).
+    // Each part starts on a wave boundary (pw = p rounded up to 64) so no wave mixes the G1 and
+    // G2 chains (a mixed wave runs both back to back): U_j at lane j, W_j at pw + j, the own
+    // share halves at 2 pw + h.
+    const uint32_t pw = (p + 63) & ~63u;
+    const uint32_t k = (bid - hash_blocks) * blockDim.x + threadIdx.x;
     if (k < p) {
       g1a u;
       int32_t st = g1_decompress(u_comp + (size_t)k * 48, u);
       if (st == HBX_PT_OK && !g1_is_torsion_free(u)) st = HBX_PT_NOT_IN_SUBGROUP;
       dec_st[k] = st;
       U[k] = u;
-    } else if (own_sk && k >= 2 * p && k < 4 * p) {
+    } else if (own_sk && k >= 2 * pw && k < 2 * pw + 2 * p) {
       // this node's own decryption share sk_me * U_j (decrypt_share_no_verify,
       // honey_badger.rs:403), GLV k = k1 + k2 lambda, phi(x, y) = (beta x, y), one half per lane:
       // lane 2j computes k1 U_j, lane 2j + 1 computes k2 phi(U_j), each decoding U_j itself so
       // neither waits for the subgroup check (k_prepare_lines adds the halves where U_j is valid)
-      const uint32_t h = k - 2 * p, j = h >> 1;
+      const uint32_t h = k - 2 * pw, j = h >> 1;
       g1a u;
       g1j part = g1_identity();
       if (g1_decompress(u_comp + (size_t)j * 48, u) == HBX_PT_OK) {
@@ -109,17 +114,17 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
         part = g1_mul_u128(u, (h & 1) ? k2 : k1);
       }
       own_part[h] = part;
-    } else if (k < 2 * p) {
-      const uint32_t j = k - p;
+    } else if (k >= pw && k < pw + p) {
+      const uint32_t j = k - pw;
       g2a w;
       int32_t st = g2_decompress(w_comp + (size_t)j * 96, w);
       if (st == HBX_PT_OK && !g2_is_torsion_free(w)) st = HBX_PT_NOT_IN_SUBGROUP;
-      dec_st[k] = st;
+      dec_st[p + j] = st;
       G2pts[2 * j + 1] = w;
     }
     return;
   }
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gid = bid * blockDim.x + threadIdx.x;
   const uint32_t j = gid / HASH_K;
   if (j >= p) return;  // whole groups only (HASH_K | 64)
   const uint64_t off = v_off[j];
@@ -321,10 +326,13 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
 }
 
+#ifndef HBX_V3_WAVES
+#define HBX_V3_WAVES 1
+#endif
 // k_verify_shares with THREE lanes per share (pairing3.hpp): 21 checks per wave, ~2.5x lower
 // latency per check.  Used when a launch has too few shares to fill the chip one lane per share
 // (an epoch shard on one of several GPUs).  Same inputs, outputs and own-share semantics.
-__global__ void __launch_bounds__(64) k_verify_shares3(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
+__global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
                                                        const uint8_t* __restrict__ present,
                                                        const g1a* __restrict__ pk, uint32_t n_keys,
                                                        const g2a* __restrict__ G2pts,
@@ -760,16 +768,55 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __rest
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
 }
 
+// lambda (canonical Fr, 8 LE limbs) in base X = |x| = 0xd201000000010000: lambda = d0 + d1 X +
+// d2 X^2 + d3 X^3 (lambda < r < X^4), by binary long division (the remainder needs 65 bits
+// between steps: its top bit is carried in `top`).
+__device__ void fr_base_x_digits(const uint32_t* lam, uint64_t* d) {
+  uint32_t v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = lam[i];
+  for (int q = 0; q < 4; q++) {
+    uint64_t rem = 0;
+    for (int bit = 255; bit >= 0; bit--) {
+      const uint32_t w = (uint32_t)bit >> 5, sh = (uint32_t)bit & 31;
+      const uint64_t top = rem >> 63;
+      rem = (rem << 1) | ((v[w] >> sh) & 1u);
+      const bool ge = top != 0 || rem >= BLS_X;
+      if (ge) rem -= BLS_X;
+      v[w] = (v[w] & ~(1u << sh)) | ((ge ? 1u : 0u) << sh);  // quotient bit replaces the dividend bit
+    }
+    d[q] = rem;
+  }
+}
+
+// g2j sum over the lanes of a block (tree: lane pairs by shuffles inside each wave, then the
+// per-wave partial sums through LDS).  Every lane must call it; the result is valid in thread 0.
+__device__ __forceinline__ fq fq_shfl_xor(const fq& a, int m) {
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__shfl_xor((int)a.l[i], m);
+  return r;
+}
+__device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
+  return g2j{fq2{fq_shfl_xor(a.x.c0, m), fq_shfl_xor(a.x.c1, m)}, fq2{fq_shfl_xor(a.y.c0, m), fq_shfl_xor(a.y.c1, m)},
+             fq2{fq_shfl_xor(a.z.c0, m), fq_shfl_xor(a.z.c1, m)}};
+}
+
 // B3: PublicKeySet::combine_signatures over the first t valid shares in node-index order
-// (common_coin.rs:190; received_shares is a BTreeMap): Lagrange at 0 in G2, one 128-thread block
-// per instance.  status: 0 or HBX_E_NOT_ENOUGH_SHARDS-style -3 (NotEnoughShares).
-constexpr int SIGCOMB_THREADS = 128;
+// (common_coin.rs:190; received_shares is a BTreeMap): sig = sum lambda_k S_k, Lagrange at 0 in
+// G2.  Each S_k is in G2 (the decode checks membership), where psi acts as [x] = [-X]; with
+// lambda_k = d0 + d1 X + d2 X^2 + d3 X^3 (|d_i| < X < 2^64),
+//     lambda_k S_k = d0 S_k - d1 psi(S_k) + d2 psi^2(S_k) - d3 psi^3(S_k),
+// four independent 64-bit scalar multiplications, one per lane (lane 4k + i), instead of one
+// 255-bit multiplication: a quarter of the doubling chain.  One block per instance.
+// status: 0 or -3 (NotEnoughShares).
+constexpr int SIGCOMB_THREADS = 256;
 __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t* __restrict__ valid,
                                                                   const g2a* __restrict__ sig, uint32_t n, uint32_t t,
                                                                   g2a* __restrict__ out, int32_t* __restrict__ status) {
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;
-  __shared__ g2j red[SIGCOMB_THREADS];
+  __shared__ g2j red[SIGCOMB_THREADS / 64];
   const uint32_t inst = blockIdx.x;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -787,43 +834,64 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
     return;
   }
   g2j acc = g2_identity();
-  for (int k = tid; k < (int)t; k += SIGCOMB_THREADS) {
+  for (int q = tid; q < 4 * (int)t; q += SIGCOMB_THREADS) {
+    const int k = q >> 2, i = q & 3;
     const fr lam = lagrange_at_zero(idx, (int)t, k);
-    acc = g2_add(acc, g2_mul_bits(g2_from_affine(sig[(size_t)inst * n + idx[k]]), lam.l, 256));
+    uint64_t d[4];
+    fr_base_x_digits(lam.l, d);
+    g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
+    for (int e = 0; e < i; e++) P = g2_psi(P);  // affine in, affine out (Z = 1)
+    g2a Pa{P.x, i & 1 ? fq2_neg(P.y) : P.y, false};
+    if (d[i] != 0) acc = g2_add(acc, g2_mul_u64_naf(Pa, d[i]));
   }
-  red[tid] = acc;
+#pragma unroll 1
+  for (int m = 1; m < 64; m <<= 1) acc = g2_add(acc, g2j_shfl_xor(acc, m));
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
   __syncthreads();
-  for (int stride = SIGCOMB_THREADS / 2; stride > 0; stride >>= 1) {
-    if (tid < stride) red[tid] = g2_add(red[tid], red[tid + stride]);
-    __syncthreads();
-  }
   if (tid == 0) {
-    out[inst] = g2_to_affine(red[0]);
+    g2j sum = red[0];
+    for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g2_add(sum, red[w]);
+    out[inst] = g2_to_affine(sum);
     status[inst] = 0;
   }
 }
 
-// B3 master check (PublicKey::verify, common_coin.rs:196) + B4 Signature::parity (:173) +
-// the compressed signature, one lane per instance.
-__global__ void __launch_bounds__(64) k_master_verify(const line_pre* __restrict__ lines, const g2a* __restrict__ H,
-                                                      const g1a* __restrict__ master_pk, const g2a* __restrict__ sig,
-                                                      const int32_t* __restrict__ status, uint32_t count,
-                                                      uint8_t* __restrict__ master_ok, uint8_t* __restrict__ parity,
-                                                      uint8_t* __restrict__ sig96) {
+// B3 master check (PublicKey::verify, common_coin.rs:196): e(master_pk, H_j) e(-g1, sig_j) == 1
+// with prepared lines for both G2 points (H_j from hbx_prepare_nonces, sig_j by k_prepare_lines),
+// three lanes per check (pairing3.hpp).  Instances whose combine failed get master_ok = 0.
+__global__ void __launch_bounds__(64) k_master_verify3(const line_pre* __restrict__ h_lines, const g2a* __restrict__ H,
+                                                       const g1a* __restrict__ master_pk,
+                                                       const line_pre* __restrict__ sig_lines, const g2a* __restrict__ sig,
+                                                       const int32_t* __restrict__ status, uint32_t count,
+                                                       uint8_t* __restrict__ master_ok) {
+  const int lane = (int)(threadIdx.x & 63);
+  const grp3 g = grp3_of_lane();
+  const uint32_t j = blockIdx.x * G3_PER_WAVE + (uint32_t)(lane / G3);
+  if (lane == 63 || j >= count) return;  // whole groups
+  bool ok = false;
+  if (status[j] == 0) {
+    g1a ng;
+    ng.x = fq_from_const(G1_GEN_X);
+    ng.y = fq_neg(fq_from_const(G1_GEN_Y));
+    ng.inf = false;
+    ok = check2_g3<false>(h_lines + (size_t)j * MILLER_LINES, master_pk[0], H[j].inf,
+                          sig_lines + (size_t)j * MILLER_LINES, ng, sig[j].inf, g);
+  }
+  if (g.gl == 0) master_ok[j] = ok ? 1 : 0;
+}
+
+// B4 Signature::parity (common_coin.rs:173) and the compressed signature, one lane per instance.
+__global__ void __launch_bounds__(64) k_sig_parity(const g2a* __restrict__ sig, const int32_t* __restrict__ status,
+                                                   uint32_t count, uint8_t* __restrict__ parity,
+                                                   uint8_t* __restrict__ sig96) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= count) return;
   if (status[j] != 0) {
-    master_ok[j] = 0;
     parity[j] = 0;
     for (int q = 0; q < 96; q++) sig96[(size_t)j * 96 + q] = 0;
     return;
   }
-  g1a ng;
-  ng.x = fq_from_const(G1_GEN_X);
-  ng.y = fq_neg(fq_from_const(G1_GEN_Y));
-  ng.inf = false;
   const g2a s = sig[j];
-  master_ok[j] = check_mixed(lines + (size_t)j * MILLER_LINES, master_pk[0], H[j].inf, s, ng) ? 1 : 0;
   uint8_t u[192];
   g2_uncompressed(s, u);
   uint8_t x = 0;

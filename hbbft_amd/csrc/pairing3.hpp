@@ -195,6 +195,9 @@ __device__ __forceinline__ bool is_one3(const fq4& a, const grp3 g) {
 }
 
 // Two Miller loops over prepared lines (pairing.hpp miller_loop2), conjugated for x < 0.
+// UNIFORM: the line arrays are the same for every group of the wave (scalar loads); otherwise
+// each group reads its own lines (vector loads).
+template <bool UNIFORM = true>
 __device__ fq4 miller3(const line_pre* LA, const g1a& PA, bool useA, const line_pre* LB, const g1a& PB, bool useB,
                        const grp3 g) {
   fq4 f = g.gl == 0 ? fq4_one() : fq4_zero();
@@ -206,7 +209,8 @@ __device__ fq4 miller3(const line_pre* LA, const g1a& PA, bool useA, const line_
 #pragma unroll 1
     for (int s = 0; s < steps; s++) {
       const bool b = (s & 1) != 0;
-      const line_pre L = ld_uniform((b ? LB : LA) + k);
+      const line_pre* lp = (b ? LB : LA) + k;
+      const line_pre L = UNIFORM ? ld_uniform(lp) : *lp;
       if (b ? useB : useA) {
         const fq px = b ? PB.x : PA.x;
         const fq py = b ? PB.y : PA.y;
@@ -248,12 +252,13 @@ __device__ __noinline__ fq4 final_exp3(const fq4& f, const grp3 g) {
 }
 
 // e(PA, QA) e(PB, QB) == 1 with identity handling (check2 of hbx_kernels.hip); group-uniform.
+template <bool UNIFORM = true>
 __device__ __forceinline__ bool check2_g3(const line_pre* LA, const g1a& PA, bool qa_inf, const line_pre* LB,
                                           const g1a& PB, bool qb_inf, const grp3 g) {
   const bool skipA = PA.inf || qa_inf;
   const bool skipB = PB.inf || qb_inf;
   if (skipA && skipB) return true;
-  const fq4 f = miller3(LA, PA, !skipA, LB, PB, !skipB, g);
+  const fq4 f = miller3<UNIFORM>(LA, PA, !skipA, LB, PB, !skipB, g);
   return is_one3(final_exp3(f, g), g);
 }
 

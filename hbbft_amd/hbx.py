@@ -13,7 +13,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhbx.so")
+# HBX_LIB_PATH: an alternative in-tree build of the same library (kernel variants under test)
+LIB_PATH = os.environ.get("HBX_LIB_PATH") or os.path.join(_HERE, "libhbx.so")
 
 HBX_OK = 0
 HBX_E_INVALID_ARG = -1
@@ -88,7 +89,7 @@ CT_UNDECODABLE = 3
 
 # kernel ids of hbx_kernel_time (include/hbx.h)
 KERNELS = {"prepare_ct": 0, "prepare_lines": 1, "ct_checks": 2, "verify_shares": 3, "combine": 4,
-           "verify_sig": 5, "combine_sigs": 6, "rs_code": 7, "merkle_leaves": 8, "hash_nonces": 9}
+           "verify_sig": 5, "combine_sigs": 6, "rs_code": 7, "merkle_leaves": 8, "hash_nonces": 9, "master_verify": 10}
 
 _lib = None
 
@@ -106,6 +107,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise OSError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same SONAME as
+    # /opt/rocm's, which libhbx.so links).  Whichever loads first serves both; if libhbx.so came
+    # first, torch later finds "No HIP GPUs".  So torch (the device-memory plumbing of the _d
+    # calls) is imported before the library whenever it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P = ctypes.c_void_p
     u8p = ctypes.POINTER(ctypes.c_uint8)
