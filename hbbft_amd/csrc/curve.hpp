@@ -47,17 +47,17 @@ HBX_HD g1j g1_from_affine(const g1a& a) {
 
 // dbl-2009-l (a = 0)
 HBX_HDNI g1j g1_dbl(const g1j& p) {
-  const fq A = fq_sqr(p.x);
-  const fq B = fq_sqr(p.y);
-  const fq C = fq_sqr(B);
-  fq D = fq_sub(fq_sub(fq_sqr(fq_add(p.x, B)), A), C);
+  const fq A = fq_sqr_inl(p.x);
+  const fq B = fq_sqr_inl(p.y);
+  const fq C = fq_sqr_inl(B);
+  fq D = fq_sub(fq_sub(fq_sqr_inl(fq_add(p.x, B)), A), C);
   D = fq_dbl(D);
   const fq E = fq_add(fq_dbl(A), A);
-  const fq F = fq_sqr(E);
+  const fq F = fq_sqr_inl(E);
   const fq X3 = fq_sub(F, fq_dbl(D));
   const fq C8 = fq_dbl(fq_dbl(fq_dbl(C)));
-  const fq Y3 = fq_sub(fq_mul(E, fq_sub(D, X3)), C8);
-  const fq Z3 = fq_dbl(fq_mul(p.y, p.z));
+  const fq Y3 = fq_sub(fq_mul_inl(E, fq_sub(D, X3)), C8);
+  const fq Z3 = fq_dbl(fq_mul_inl(p.y, p.z));
   return g1j{X3, Y3, Z3};
 }
 
@@ -65,24 +65,24 @@ HBX_HDNI g1j g1_dbl(const g1j& p) {
 HBX_HDNI g1j g1_add(const g1j& p, const g1j& q) {
   if (g1j_is_identity(p)) return q;
   if (g1j_is_identity(q)) return p;
-  const fq Z1Z1 = fq_sqr(p.z);
-  const fq Z2Z2 = fq_sqr(q.z);
-  const fq U1 = fq_mul(p.x, Z2Z2);
-  const fq U2 = fq_mul(q.x, Z1Z1);
-  const fq S1 = fq_mul(fq_mul(p.y, q.z), Z2Z2);
-  const fq S2 = fq_mul(fq_mul(q.y, p.z), Z1Z1);
+  const fq Z1Z1 = fq_sqr_inl(p.z);
+  const fq Z2Z2 = fq_sqr_inl(q.z);
+  const fq U1 = fq_mul_inl(p.x, Z2Z2);
+  const fq U2 = fq_mul_inl(q.x, Z1Z1);
+  const fq S1 = fq_mul_inl(fq_mul_inl(p.y, q.z), Z2Z2);
+  const fq S2 = fq_mul_inl(fq_mul_inl(q.y, p.z), Z1Z1);
   if (fq_eq(U1, U2)) {
     if (fq_eq(S1, S2)) return g1_dbl(p);
     return g1_identity();
   }
   const fq H = fq_sub(U2, U1);
-  const fq I = fq_sqr(fq_dbl(H));
-  const fq J = fq_mul(H, I);
+  const fq I = fq_sqr_inl(fq_dbl(H));
+  const fq J = fq_mul_inl(H, I);
   const fq r = fq_dbl(fq_sub(S2, S1));
-  const fq V = fq_mul(U1, I);
-  const fq X3 = fq_sub(fq_sub(fq_sqr(r), J), fq_dbl(V));
-  const fq Y3 = fq_sub(fq_mul(r, fq_sub(V, X3)), fq_dbl(fq_mul(S1, J)));
-  const fq Z3 = fq_mul(fq_sub(fq_sub(fq_sqr(fq_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  const fq V = fq_mul_inl(U1, I);
+  const fq X3 = fq_sub(fq_sub(fq_sqr_inl(r), J), fq_dbl(V));
+  const fq Y3 = fq_sub(fq_mul_inl(r, fq_sub(V, X3)), fq_dbl(fq_mul_inl(S1, J)));
+  const fq Z3 = fq_mul_inl(fq_sub(fq_sub(fq_sqr_inl(fq_add(p.z, q.z)), Z1Z1), Z2Z2), H);
   return g1j{X3, Y3, Z3};
 }
 
@@ -122,22 +122,22 @@ HBX_HDNI g1j g1_mul_scalar(const g1j& p, const uint32_t* k8) {
 HBX_HD g1j g1_add_mixed_i(const g1j& p, const g1a& q) {
   if (q.inf) return p;
   if (g1j_is_identity(p)) return g1j{q.x, q.y, fq_one()};
-  const fq Z1Z1 = fq_sqr(p.z);
-  const fq U2 = fq_mul(q.x, Z1Z1);
-  const fq S2 = fq_mul(fq_mul(q.y, p.z), Z1Z1);
+  const fq Z1Z1 = fq_sqr_inl(p.z);
+  const fq U2 = fq_mul_inl(q.x, Z1Z1);
+  const fq S2 = fq_mul_inl(fq_mul_inl(q.y, p.z), Z1Z1);
   const fq H = fq_sub(U2, p.x);
   const fq r = fq_dbl(fq_sub(S2, p.y));
   if (fq_is_zero(H)) {
     if (fq_is_zero(r)) return g1_dbl(p);
     return g1_identity();
   }
-  const fq HH = fq_sqr(H);
+  const fq HH = fq_sqr_inl(H);
   const fq I = fq_dbl(fq_dbl(HH));
-  const fq J = fq_mul(H, I);
-  const fq V = fq_mul(p.x, I);
-  const fq X3 = fq_sub(fq_sub(fq_sqr(r), J), fq_dbl(V));
-  const fq Y3 = fq_sub(fq_mul(r, fq_sub(V, X3)), fq_dbl(fq_mul(p.y, J)));
-  const fq Z3 = fq_sub(fq_sub(fq_sqr(fq_add(p.z, H)), Z1Z1), HH);
+  const fq J = fq_mul_inl(H, I);
+  const fq V = fq_mul_inl(p.x, I);
+  const fq X3 = fq_sub(fq_sub(fq_sqr_inl(r), J), fq_dbl(V));
+  const fq Y3 = fq_sub(fq_mul_inl(r, fq_sub(V, X3)), fq_dbl(fq_mul_inl(p.y, J)));
+  const fq Z3 = fq_sub(fq_sub(fq_sqr_inl(fq_add(p.z, H)), Z1Z1), HH);
   return g1j{X3, Y3, Z3};
 }
 
@@ -274,41 +274,41 @@ HBX_HD g2j g2_from_affine(const g2a& a) {
 }
 
 HBX_HDNI g2j g2_dbl(const g2j& p) {
-  const fq2 A = fq2_sqr(p.x);
-  const fq2 B = fq2_sqr(p.y);
-  const fq2 C = fq2_sqr(B);
-  fq2 D = fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.x, B)), A), C);
+  const fq2 A = fq2_sqr_t<FqInl>(p.x);
+  const fq2 B = fq2_sqr_t<FqInl>(p.y);
+  const fq2 C = fq2_sqr_t<FqInl>(B);
+  fq2 D = fq2_sub(fq2_sub(fq2_sqr_t<FqInl>(fq2_add(p.x, B)), A), C);
   D = fq2_dbl(D);
   const fq2 E = fq2_add(fq2_dbl(A), A);
-  const fq2 F = fq2_sqr(E);
+  const fq2 F = fq2_sqr_t<FqInl>(E);
   const fq2 X3 = fq2_sub(F, fq2_dbl(D));
   const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
-  const fq2 Y3 = fq2_sub(fq2_mul(E, fq2_sub(D, X3)), C8);
-  const fq2 Z3 = fq2_dbl(fq2_mul(p.y, p.z));
+  const fq2 Y3 = fq2_sub(fq2_mul_t<FqInl>(E, fq2_sub(D, X3)), C8);
+  const fq2 Z3 = fq2_dbl(fq2_mul_t<FqInl>(p.y, p.z));
   return g2j{X3, Y3, Z3};
 }
 
 HBX_HDNI g2j g2_add(const g2j& p, const g2j& q) {
   if (g2j_is_identity(p)) return q;
   if (g2j_is_identity(q)) return p;
-  const fq2 Z1Z1 = fq2_sqr(p.z);
-  const fq2 Z2Z2 = fq2_sqr(q.z);
-  const fq2 U1 = fq2_mul(p.x, Z2Z2);
-  const fq2 U2 = fq2_mul(q.x, Z1Z1);
-  const fq2 S1 = fq2_mul(fq2_mul(p.y, q.z), Z2Z2);
-  const fq2 S2 = fq2_mul(fq2_mul(q.y, p.z), Z1Z1);
+  const fq2 Z1Z1 = fq2_sqr_t<FqInl>(p.z);
+  const fq2 Z2Z2 = fq2_sqr_t<FqInl>(q.z);
+  const fq2 U1 = fq2_mul_t<FqInl>(p.x, Z2Z2);
+  const fq2 U2 = fq2_mul_t<FqInl>(q.x, Z1Z1);
+  const fq2 S1 = fq2_mul_t<FqInl>(fq2_mul_t<FqInl>(p.y, q.z), Z2Z2);
+  const fq2 S2 = fq2_mul_t<FqInl>(fq2_mul_t<FqInl>(q.y, p.z), Z1Z1);
   if (fq2_eq(U1, U2)) {
     if (fq2_eq(S1, S2)) return g2_dbl(p);
     return g2_identity();
   }
   const fq2 H = fq2_sub(U2, U1);
-  const fq2 I = fq2_sqr(fq2_dbl(H));
-  const fq2 J = fq2_mul(H, I);
+  const fq2 I = fq2_sqr_t<FqInl>(fq2_dbl(H));
+  const fq2 J = fq2_mul_t<FqInl>(H, I);
   const fq2 r = fq2_dbl(fq2_sub(S2, S1));
-  const fq2 V = fq2_mul(U1, I);
-  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr(r), J), fq2_dbl(V));
-  const fq2 Y3 = fq2_sub(fq2_mul(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul(S1, J)));
-  const fq2 Z3 = fq2_mul(fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  const fq2 V = fq2_mul_t<FqInl>(U1, I);
+  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr_t<FqInl>(r), J), fq2_dbl(V));
+  const fq2 Y3 = fq2_sub(fq2_mul_t<FqInl>(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul_t<FqInl>(S1, J)));
+  const fq2 Z3 = fq2_mul_t<FqInl>(fq2_sub(fq2_sub(fq2_sqr_t<FqInl>(fq2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
   return g2j{X3, Y3, Z3};
 }
 
@@ -318,22 +318,22 @@ HBX_HD g2j g2_neg(const g2j& p) { return g2j{p.x, fq2_neg(p.y), p.z}; }
 HBX_HDNI g2j g2_add_mixed(const g2j& p, const g2a& q) {
   if (q.inf) return p;
   if (g2j_is_identity(p)) return g2j{q.x, q.y, fq2_one()};
-  const fq2 Z1Z1 = fq2_sqr(p.z);
-  const fq2 U2 = fq2_mul(q.x, Z1Z1);
-  const fq2 S2 = fq2_mul(fq2_mul(q.y, p.z), Z1Z1);
+  const fq2 Z1Z1 = fq2_sqr_t<FqInl>(p.z);
+  const fq2 U2 = fq2_mul_t<FqInl>(q.x, Z1Z1);
+  const fq2 S2 = fq2_mul_t<FqInl>(fq2_mul_t<FqInl>(q.y, p.z), Z1Z1);
   if (fq2_eq(p.x, U2)) {
     if (fq2_eq(p.y, S2)) return g2_dbl(p);
     return g2_identity();
   }
   const fq2 H = fq2_sub(U2, p.x);
-  const fq2 HH = fq2_sqr(H);
+  const fq2 HH = fq2_sqr_t<FqInl>(H);
   const fq2 I = fq2_dbl(fq2_dbl(HH));
-  const fq2 J = fq2_mul(H, I);
+  const fq2 J = fq2_mul_t<FqInl>(H, I);
   const fq2 r = fq2_dbl(fq2_sub(S2, p.y));
-  const fq2 V = fq2_mul(p.x, I);
-  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr(r), J), fq2_dbl(V));
-  const fq2 Y3 = fq2_sub(fq2_mul(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul(p.y, J)));
-  const fq2 Z3 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(p.z, H)), Z1Z1), HH);
+  const fq2 V = fq2_mul_t<FqInl>(p.x, I);
+  const fq2 X3 = fq2_sub(fq2_sub(fq2_sqr_t<FqInl>(r), J), fq2_dbl(V));
+  const fq2 Y3 = fq2_sub(fq2_mul_t<FqInl>(r, fq2_sub(V, X3)), fq2_dbl(fq2_mul_t<FqInl>(p.y, J)));
+  const fq2 Z3 = fq2_sub(fq2_sub(fq2_sqr_t<FqInl>(fq2_add(p.z, H)), Z1Z1), HH);
   return g2j{X3, Y3, Z3};
 }
 

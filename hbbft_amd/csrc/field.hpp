@@ -130,7 +130,7 @@ HBX_HD void fq_unpack28(const fq& a, uint32_t* d) {
 #define HBX_P12(x)                                                                                  \
   uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6, \
       uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
-HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
+HBX_HD fq fq_mul_body(HBX_P12(a), HBX_P12(b)) {
   const fq a = {{HBX_L12(a)}};
   const fq b = {{HBX_L12(b)}};
   uint32_t A[14], B[14], m[14], o[15];
@@ -195,7 +195,7 @@ HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) {
 // taken once per pair, sum_{i<j} (2 a_i) a_j + a_{k/2}^2, i.e. 105 instead of 196 digit products
 // (the reduction's 196 m*p products are unchanged): 301 v_mad_u64_u32 instead of 392.
 // (2 a_i) < 2^29, so a column holds < 8 * 2^57 from the square plus < 14 * 2^56 from m*p.
-HBX_FQMUL_ATTR fq fq_sqr_limbs(HBX_P12(a)) {
+HBX_HD fq fq_sqr_body(HBX_P12(a)) {
   const fq a = {{HBX_L12(a)}};
   uint32_t A[14], A2[14], m[14], o[15];
   fq_unpack28(a, A);
@@ -295,6 +295,29 @@ inline fq fq_mul_cios64(const fq& a, const fq& b) {
   return r;
 }
 #endif
+// The out-of-line copies (one each on the device): called from everything that is not a hot
+// inner loop, which keeps the code of the rarely-run paths small.
+HBX_FQMUL_ATTR fq fq_mul_limbs(HBX_P12(a), HBX_P12(b)) { return fq_mul_body(HBX_L12(a), HBX_L12(b)); }
+HBX_FQMUL_ATTR fq fq_sqr_limbs(HBX_P12(a)) { return fq_sqr_body(HBX_L12(a)); }
+// Inlined copies for the hot loops (the Miller loop, the cyclotomic squarings): a call costs a
+// wave far more than its argument moves at one wave per SIMD -- the s_waitcnt at the callee's
+// entry, two jumps, and no overlap of the product with the caller's independent work
+// (tools/microbench/parts.hip: 1.50 -> 1.00 us per dependent product, Miller loop -13 %).
+HBX_HD fq fq_mul_inl(const fq& a, const fq& b) {
+  HBX_COUNT_FQMUL();
+#if defined(HBX_HOST_INT128) && !defined(__HIPCC__)
+  return fq_mul_cios64(a, b);
+#endif
+  return fq_mul_body(a.l[0], a.l[1], a.l[2], a.l[3], a.l[4], a.l[5], a.l[6], a.l[7], a.l[8], a.l[9], a.l[10], a.l[11],
+                     b.l[0], b.l[1], b.l[2], b.l[3], b.l[4], b.l[5], b.l[6], b.l[7], b.l[8], b.l[9], b.l[10], b.l[11]);
+}
+HBX_HD fq fq_sqr_inl(const fq& a) {
+  HBX_COUNT_FQMUL();
+#if defined(HBX_HOST_INT128) && !defined(__HIPCC__)
+  return fq_mul_cios64(a, a);
+#endif
+  return fq_sqr_body(a.l[0], a.l[1], a.l[2], a.l[3], a.l[4], a.l[5], a.l[6], a.l[7], a.l[8], a.l[9], a.l[10], a.l[11]);
+}
 HBX_HD fq fq_mul(const fq& a, const fq& b) {
   HBX_COUNT_FQMUL();
 #if defined(HBX_HOST_INT128) && !defined(__HIPCC__)
@@ -419,17 +442,15 @@ HBX_HDNI fq fq_pow_const(const fq& a, const uint32_t* e) {
   for (int w = 95; w >= 0; w--) {
     const uint32_t nib = (e[w >> 3] >> ((w & 7) * 4)) & 0xF;
     if (started) {
-      r = fq_sqr(r);
-      r = fq_sqr(r);
-      r = fq_sqr(r);
-      r = fq_sqr(r);
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) r = fq_sqr_inl(r);
     }
     if (nib) {
       // select tab[nib] without dynamic register indexing
       fq t = tab[1];
       for (int k = 2; k < 16; k++)
         if ((uint32_t)k == nib) t = tab[k];
-      r = started ? fq_mul(r, t) : t;
+      r = started ? fq_mul_inl(r, t) : t;
       started = true;
     }
   }
@@ -576,19 +597,38 @@ HBX_HD fq2 fq2_neg(const fq2& a) { return fq2{fq_neg(a.c0), fq_neg(a.c1)}; }
 HBX_HD fq2 fq2_dbl(const fq2& a) { return fq2{fq_dbl(a.c0), fq_dbl(a.c1)}; }
 HBX_HD fq2 fq2_conj(const fq2& a) { return fq2{a.c0, fq_neg(a.c1)}; }
 
-HBX_HD fq2 fq2_mul(const fq2& a, const fq2& b) {
-  const fq t0 = fq_mul(a.c0, b.c0);
-  const fq t1 = fq_mul(a.c1, b.c1);
-  const fq t2 = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
+// Product policy of the tower templates below: FqCall = the out-of-line Fq product (compact code),
+// FqInl = the inlined one (hot loops).  Same values either way.
+struct FqCall {
+  static HBX_HD fq mul(const fq& a, const fq& b) { return fq_mul(a, b); }
+  static HBX_HD fq sqr(const fq& a) { return fq_sqr(a); }
+};
+struct FqInl {
+  static HBX_HD fq mul(const fq& a, const fq& b) { return fq_mul_inl(a, b); }
+  static HBX_HD fq sqr(const fq& a) { return fq_sqr_inl(a); }
+};
+
+template <class M>
+HBX_HD fq2 fq2_mul_t(const fq2& a, const fq2& b) {
+  const fq t0 = M::mul(a.c0, b.c0);
+  const fq t1 = M::mul(a.c1, b.c1);
+  const fq t2 = M::mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
   return fq2{fq_sub(t0, t1), fq_sub(fq_sub(t2, t0), t1)};
 }
-HBX_HD fq2 fq2_sqr(const fq2& a) {
+template <class M>
+HBX_HD fq2 fq2_sqr_t(const fq2& a) {
   // (a0 + a1)(a0 - a1), 2 a0 a1
-  const fq t0 = fq_mul(fq_add(a.c0, a.c1), fq_sub(a.c0, a.c1));
-  const fq t1 = fq_mul(a.c0, a.c1);
+  const fq t0 = M::mul(fq_add(a.c0, a.c1), fq_sub(a.c0, a.c1));
+  const fq t1 = M::mul(a.c0, a.c1);
   return fq2{t0, fq_dbl(t1)};
 }
-HBX_HD fq2 fq2_mul_fq(const fq2& a, const fq& s) { return fq2{fq_mul(a.c0, s), fq_mul(a.c1, s)}; }
+template <class M>
+HBX_HD fq2 fq2_mul_fq_t(const fq2& a, const fq& s) { return fq2{M::mul(a.c0, s), M::mul(a.c1, s)}; }
+HBX_HD fq2 fq2_mul(const fq2& a, const fq2& b) { return fq2_mul_t<FqCall>(a, b); }
+HBX_HD fq2 fq2_sqr(const fq2& a) {
+  return fq2_sqr_t<FqCall>(a);
+}
+HBX_HD fq2 fq2_mul_fq(const fq2& a, const fq& s) { return fq2_mul_fq_t<FqCall>(a, s); }
 // multiply by the Fq6 non-residue xi = 1 + u
 HBX_HD fq2 fq2_mul_xi(const fq2& a) { return fq2{fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1)}; }
 HBX_HD bool fq2_is_zero(const fq2& a) { return fq_is_zero(a.c0) && fq_is_zero(a.c1); }
@@ -672,21 +712,23 @@ HBX_HD fq6 fq6_neg(const fq6& a) { return fq6{fq2_neg(a.c0), fq2_neg(a.c1), fq2_
 HBX_HD fq6 fq6_mul_v(const fq6& a) { return fq6{fq2_mul_xi(a.c2), a.c0, a.c1}; }
 
 // Karatsuba-style Fq6 product (6 Fq2 mults).
-HBX_HD fq6 fq6_mul_i(const fq6& a, const fq6& b) {
-  const fq2 t0 = fq2_mul(a.c0, b.c0);
-  const fq2 t1 = fq2_mul(a.c1, b.c1);
-  const fq2 t2 = fq2_mul(a.c2, b.c2);
+template <class M>
+HBX_HD fq6 fq6_mul_t(const fq6& a, const fq6& b) {
+  const fq2 t0 = fq2_mul_t<M>(a.c0, b.c0);
+  const fq2 t1 = fq2_mul_t<M>(a.c1, b.c1);
+  const fq2 t2 = fq2_mul_t<M>(a.c2, b.c2);
   // c0 = t0 + xi((a1+a2)(b1+b2) - t1 - t2)
-  fq2 c0 = fq2_mul(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2));
+  fq2 c0 = fq2_mul_t<M>(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2));
   c0 = fq2_add(t0, fq2_mul_xi(fq2_sub(fq2_sub(c0, t1), t2)));
   // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
-  fq2 c1 = fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1));
+  fq2 c1 = fq2_mul_t<M>(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1));
   c1 = fq2_add(fq2_sub(fq2_sub(c1, t0), t1), fq2_mul_xi(t2));
   // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
-  fq2 c2 = fq2_mul(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2));
+  fq2 c2 = fq2_mul_t<M>(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2));
   c2 = fq2_add(fq2_sub(fq2_sub(c2, t0), t2), t1);
   return fq6{c0, c1, c2};
 }
+HBX_HD fq6 fq6_mul_i(const fq6& a, const fq6& b) { return fq6_mul_t<FqCall>(a, b); }
 HBX_HDNI fq6 fq6_mul(const fq6& a, const fq6& b) { return fq6_mul_i(a, b); }
 
 HBX_HD fq6 fq6_sqr_i(const fq6& a) {
@@ -706,23 +748,27 @@ HBX_HD fq6 fq6_sqr_i(const fq6& a) {
 HBX_HDNI fq6 fq6_sqr(const fq6& a) { return fq6_sqr_i(a); }
 
 // a * (b0 + b1 v)   (5 Fq2 mults)
-HBX_HD fq6 fq6_mul_by_01_i(const fq6& a, const fq2& b0, const fq2& b1) {
-  const fq2 t0 = fq2_mul(a.c0, b0);
-  const fq2 t1 = fq2_mul(a.c1, b1);
+template <class M>
+HBX_HD fq6 fq6_mul_by_01_t(const fq6& a, const fq2& b0, const fq2& b1) {
+  const fq2 t0 = fq2_mul_t<M>(a.c0, b0);
+  const fq2 t1 = fq2_mul_t<M>(a.c1, b1);
   // c0 = t0 + xi * (a2 * b1)
-  const fq2 c0 = fq2_add(t0, fq2_mul_xi(fq2_mul(a.c2, b1)));
+  const fq2 c0 = fq2_add(t0, fq2_mul_xi(fq2_mul_t<M>(a.c2, b1)));
   // c1 = (a0 + a1)(b0 + b1) - t0 - t1
-  const fq2 c1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b0, b1)), t0), t1);
+  const fq2 c1 = fq2_sub(fq2_sub(fq2_mul_t<M>(fq2_add(a.c0, a.c1), fq2_add(b0, b1)), t0), t1);
   // c2 = a2 * b0 + t1
-  const fq2 c2 = fq2_add(fq2_mul(a.c2, b0), t1);
+  const fq2 c2 = fq2_add(fq2_mul_t<M>(a.c2, b0), t1);
   return fq6{c0, c1, c2};
 }
+HBX_HD fq6 fq6_mul_by_01_i(const fq6& a, const fq2& b0, const fq2& b1) { return fq6_mul_by_01_t<FqCall>(a, b0, b1); }
 HBX_HDNI fq6 fq6_mul_by_01(const fq6& a, const fq2& b0, const fq2& b1) { return fq6_mul_by_01_i(a, b0, b1); }
 
 // a * (s v) with s in Fq: (xi a2 s, a0 s, a1 s)
-HBX_HD fq6 fq6_mul_by_1_fq(const fq6& a, const fq& s) {
-  return fq6{fq2_mul_xi(fq2_mul_fq(a.c2, s)), fq2_mul_fq(a.c0, s), fq2_mul_fq(a.c1, s)};
+template <class M>
+HBX_HD fq6 fq6_mul_by_1_fq_t(const fq6& a, const fq& s) {
+  return fq6{fq2_mul_xi(fq2_mul_fq_t<M>(a.c2, s)), fq2_mul_fq_t<M>(a.c0, s), fq2_mul_fq_t<M>(a.c1, s)};
 }
+HBX_HD fq6 fq6_mul_by_1_fq(const fq6& a, const fq& s) { return fq6_mul_by_1_fq_t<FqCall>(a, s); }
 
 HBX_HDNI fq6 fq6_inv(const fq6& a) {
   const fq2 c0 = fq2_sub(fq2_sqr(a.c0), fq2_mul_xi(fq2_mul(a.c1, a.c2)));
@@ -747,26 +793,32 @@ HBX_HD fq12 fq12_mul_i(const fq12& a, const fq12& b) {
 }
 HBX_HDNI fq12 fq12_mul(const fq12& a, const fq12& b) { return fq12_mul_i(a, b); }
 
-HBX_HD fq12 fq12_sqr_i(const fq12& a) {
+template <class M>
+HBX_HD fq12 fq12_sqr_t(const fq12& a) {
   // complex squaring: c0 = (a0 + a1)(a0 + v a1) - ab - v ab, c1 = 2 ab
-  const fq6 ab = fq6_mul_i(a.c0, a.c1);
-  const fq6 t = fq6_mul_i(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));
+  const fq6 ab = fq6_mul_t<M>(a.c0, a.c1);
+  const fq6 t = fq6_mul_t<M>(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));
   const fq6 c0 = fq6_sub(fq6_sub(t, ab), fq6_mul_v(ab));
   return fq12{c0, fq6_add(ab, ab)};
 }
+HBX_HD fq12 fq12_sqr_i(const fq12& a) { return fq12_sqr_t<FqCall>(a); }
 HBX_HDNI fq12 fq12_sqr(const fq12& a) { return fq12_sqr_i(a); }
 
 // f * (c0 + c1 v + c4 v w) with c0, c1 in Fq2 and c4 in Fq -- the shape of a prepared line
 // evaluated at a G1 point (pairing's mul_by_014, with c4 real).
-HBX_HD fq12 fq12_mul_by_014_i(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
-  const fq6 aa = fq6_mul_by_01_i(f.c0, c0, c1);
-  const fq6 bb = fq6_mul_by_1_fq(f.c1, c4);
+template <class M>
+HBX_HD fq12 fq12_mul_by_014_t(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
+  const fq6 aa = fq6_mul_by_01_t<M>(f.c0, c0, c1);
+  const fq6 bb = fq6_mul_by_1_fq_t<M>(f.c1, c4);
   const fq2 o = fq2{fq_add(c1.c0, c4), c1.c1};
   fq6 s = fq6_add(f.c1, f.c0);
-  s = fq6_mul_by_01_i(s, c0, o);
+  s = fq6_mul_by_01_t<M>(s, c0, o);
   const fq6 n1 = fq6_sub(fq6_sub(s, aa), bb);
   const fq6 n0 = fq6_add(fq6_mul_v(bb), aa);
   return fq12{n0, n1};
+}
+HBX_HD fq12 fq12_mul_by_014_i(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) {
+  return fq12_mul_by_014_t<FqCall>(f, c0, c1, c4);
 }
 HBX_HDNI fq12 fq12_mul_by_014(const fq12& f, const fq2& c0, const fq2& c1, const fq& c4) { return fq12_mul_by_014_i(f, c0, c1, c4); }
 
@@ -805,23 +857,26 @@ HBX_HDNI fq12 fq12_frobenius2(const fq12& a) {
 }
 
 // Granger-Scott squaring, valid in the cyclotomic subgroup (after the easy part).
-HBX_HD void fq4_sqr(const fq2& a, const fq2& b, fq2& c0, fq2& c1) {
-  const fq2 t0 = fq2_sqr(a);
-  const fq2 t1 = fq2_sqr(b);
+template <class M>
+HBX_HD void fq4_sqr_t(const fq2& a, const fq2& b, fq2& c0, fq2& c1) {
+  const fq2 t0 = fq2_sqr_t<M>(a);
+  const fq2 t1 = fq2_sqr_t<M>(b);
   c0 = fq2_add(fq2_mul_xi(t1), t0);
-  c1 = fq2_sub(fq2_sub(fq2_sqr(fq2_add(a, b)), t0), t1);
+  c1 = fq2_sub(fq2_sub(fq2_sqr_t<M>(fq2_add(a, b)), t0), t1);
 }
-HBX_HD fq12 fq12_cyclotomic_sqr_i(const fq12& f) {
+HBX_HD void fq4_sqr(const fq2& a, const fq2& b, fq2& c0, fq2& c1) { fq4_sqr_t<FqCall>(a, b, c0, c1); }
+template <class M>
+HBX_HD fq12 fq12_cyclotomic_sqr_t(const fq12& f) {
   fq2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
   fq2 z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   fq2 t0, t1, t2, t3;
-  fq4_sqr(z0, z1, t0, t1);
+  fq4_sqr_t<M>(z0, z1, t0, t1);
   z0 = fq2_sub(t0, z0);
   z0 = fq2_add(fq2_dbl(z0), t0);
   z1 = fq2_add(t1, z1);
   z1 = fq2_add(fq2_dbl(z1), t1);
-  fq4_sqr(z2, z3, t0, t1);
-  fq4_sqr(z4, z5, t2, t3);
+  fq4_sqr_t<M>(z2, z3, t0, t1);
+  fq4_sqr_t<M>(z4, z5, t2, t3);
   z4 = fq2_sub(t0, z4);
   z4 = fq2_add(fq2_dbl(z4), t0);
   z5 = fq2_add(t1, z5);
@@ -833,6 +888,7 @@ HBX_HD fq12 fq12_cyclotomic_sqr_i(const fq12& f) {
   z3 = fq2_add(fq2_dbl(z3), t2);
   return fq12{fq6{z0, z4, z3}, fq6{z2, z1, z5}};
 }
+HBX_HD fq12 fq12_cyclotomic_sqr_i(const fq12& f) { return fq12_cyclotomic_sqr_t<FqCall>(f); }
 HBX_HDNI fq12 fq12_cyclotomic_sqr(const fq12& f) { return fq12_cyclotomic_sqr_i(f); }
 
 HBX_HD bool fq12_is_one(const fq12& a) {

@@ -312,6 +312,17 @@ __device__ __forceinline__ fq fq_from_lane(const fq& v, int src) {
   for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__shfl((int)v.l[i], src, 64);
   return r;
 }
+// Lane K of the calling lane's 16-lane row (= its group: groups here are 16 aligned lanes), to
+// every lane of the row: a DPP row_newbcast move per limb -- VALU, no LDS round trip as with
+// __shfl.  K must be a constant; all 16 lanes of the row must be active.
+template <int K>
+__device__ __forceinline__ fq fq_from_row(const fq& v) {
+  static_assert(K >= 0 && K < 16, "row lane");
+  fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.l[i], 0x150 + K, 0xf, 0xf, false);
+  return r;
+}
 __device__ __forceinline__ fq fq_sel8(int s, const fq& v0, const fq& v1, const fq& v2, const fq& v3, const fq& v4,
                                       const fq& v5, const fq& v6, const fq& v7) {
   fq r;
@@ -335,32 +346,32 @@ __device__ __forceinline__ fq fq_sel16(int s, const fq (&v)[16]) {
   return r;
 }
 
-__device__ __noinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
+__device__ __forceinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
   const int s = gl & 7;
   const fq x0 = p.x.c0, x1 = p.x.c1, y0 = p.y.c0, y1 = p.y.c1, z0 = p.z.c0, z1 = p.z.c1;
   // round 1: A = X^2 (lanes 0, 1), B = Y^2 (2, 3), Y Z (4..7)
-  fq r = fq_mul(fq_sel8(s, fq_add(x0, x1), x0, fq_add(y0, y1), y0, y0, y1, y0, y1),
+  fq r = fq_mul_inl(fq_sel8(s, fq_add(x0, x1), x0, fq_add(y0, y1), y0, y0, y1, y0, y1),
                 fq_sel8(s, fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, z0, z1, z1, z0));
-  const fq2 A = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
-  const fq2 B = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
-  const fq2 YZ = fq2{fq_sub(fq_from_lane(r, gbase + 4), fq_from_lane(r, gbase + 5)),
-                     fq_add(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7))};
+  const fq2 A = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
+  const fq2 B = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
+  const fq2 YZ = fq2{fq_sub(fq_from_row<4>(r), fq_from_row<5>(r)),
+                     fq_add(fq_from_row<6>(r), fq_from_row<7>(r))};
   // round 2: C = B^2 (0, 1), T = (X + B)^2 (2, 3), F = E^2 with E = 3A (4, 5)
   const fq2 S = fq2_add(p.x, B);
   const fq2 E = fq2_add(fq2_dbl(A), A);
-  r = fq_mul(fq_sel8(s, fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0, E.c0, E.c0),
+  r = fq_mul_inl(fq_sel8(s, fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0, E.c0, E.c0),
              fq_sel8(s, fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1, E.c1, E.c1));
-  const fq2 C = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
-  const fq2 T = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
-  const fq2 F = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
+  const fq2 C = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
+  const fq2 T = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
+  const fq2 F = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
   const fq2 D = fq2_dbl(fq2_sub(fq2_sub(T, A), C));
   const fq2 X3 = fq2_sub(F, fq2_dbl(D));
   // round 3: E (D - X3) (0..3)
   const fq2 G = fq2_sub(D, X3);
-  r = fq_mul(fq_sel8(s, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1),
+  r = fq_mul_inl(fq_sel8(s, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1),
              fq_sel8(s, G.c0, G.c1, G.c1, G.c0, G.c0, G.c1, G.c1, G.c0));
-  const fq2 EG = fq2{fq_sub(fq_from_lane(r, gbase + 0), fq_from_lane(r, gbase + 1)),
-                     fq_add(fq_from_lane(r, gbase + 2), fq_from_lane(r, gbase + 3))};
+  const fq2 EG = fq2{fq_sub(fq_from_row<0>(r), fq_from_row<1>(r)),
+                     fq_add(fq_from_row<2>(r), fq_from_row<3>(r))};
   const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
   return g2j{X3, fq2_sub(EG, C8), fq2_dbl(YZ)};
 }
@@ -384,13 +395,14 @@ __device__ __forceinline__ void r16_sqr(round16& R, int k, const fq2& x) {
   R.a[k] = fq_add(x.c0, x.c1); R.b[k] = fq_sub(x.c0, x.c1);
   R.a[k + 1] = x.c0; R.b[k + 1] = x.c1;
 }
-__device__ __forceinline__ fq r16_run(const round16& R, int gl) { return fq_mul(fq_sel16(gl, R.a), fq_sel16(gl, R.b)); }
-__device__ __forceinline__ fq2 r16_get_mul(const fq& r, int k, int gbase) {
-  return fq2{fq_sub(fq_from_lane(r, gbase + k), fq_from_lane(r, gbase + k + 1)),
-             fq_add(fq_from_lane(r, gbase + k + 2), fq_from_lane(r, gbase + k + 3))};
+__device__ __forceinline__ fq r16_run(const round16& R, int gl) { return fq_mul_inl(fq_sel16(gl, R.a), fq_sel16(gl, R.b)); }
+template <int K>
+__device__ __forceinline__ fq2 r16_get_mul(const fq& r) {
+  return fq2{fq_sub(fq_from_row<K>(r), fq_from_row<K + 1>(r)), fq_add(fq_from_row<K + 2>(r), fq_from_row<K + 3>(r))};
 }
-__device__ __forceinline__ fq2 r16_get_sqr(const fq& r, int k, int gbase) {
-  return fq2{fq_from_lane(r, gbase + k), fq_dbl(fq_from_lane(r, gbase + k + 1))};
+template <int K>
+__device__ __forceinline__ fq2 r16_get_sqr(const fq& r) {
+  return fq2{fq_from_row<K>(r), fq_dbl(fq_from_row<K + 1>(r))};
 }
 __device__ __forceinline__ void r16_clear(round16& R) {
 #pragma unroll
@@ -411,17 +423,17 @@ __device__ __noinline__ g2j g2_add_group(const g2j& p, const g2j& q, int gl, int
   r16_mul(R, 8, q.y, p.z);
   r16_sqr(R, 12, fq2_add(p.z, q.z));
   fq r = r16_run(R, gl);
-  const fq2 Z1Z1 = r16_get_sqr(r, 0, gbase), Z2Z2 = r16_get_sqr(r, 2, gbase);
-  const fq2 Y1Z2 = r16_get_mul(r, 4, gbase), Y2Z1 = r16_get_mul(r, 8, gbase);
-  const fq2 ZS = r16_get_sqr(r, 12, gbase);
+  const fq2 Z1Z1 = r16_get_sqr<0>(r), Z2Z2 = r16_get_sqr<2>(r);
+  const fq2 Y1Z2 = r16_get_mul<4>(r), Y2Z1 = r16_get_mul<8>(r);
+  const fq2 ZS = r16_get_sqr<12>(r);
   // round 2: U1, U2, S1, S2
   r16_mul(R, 0, p.x, Z2Z2);
   r16_mul(R, 4, q.x, Z1Z1);
   r16_mul(R, 8, Y1Z2, Z2Z2);
   r16_mul(R, 12, Y2Z1, Z1Z1);
   r = r16_run(R, gl);
-  const fq2 U1 = r16_get_mul(r, 0, gbase), U2 = r16_get_mul(r, 4, gbase);
-  const fq2 S1 = r16_get_mul(r, 8, gbase), S2 = r16_get_mul(r, 12, gbase);
+  const fq2 U1 = r16_get_mul<0>(r), U2 = r16_get_mul<4>(r);
+  const fq2 S1 = r16_get_mul<8>(r), S2 = r16_get_mul<12>(r);
   if (fq2_eq(U1, U2)) {
     if (fq2_eq(S1, S2)) return g2_dbl_group(p, gl, gbase);
     return g2_identity();
@@ -433,18 +445,18 @@ __device__ __noinline__ g2j g2_add_group(const g2j& p, const g2j& q, int gl, int
   r16_sqr(R, 2, rr);
   r16_mul(R, 4, fq2_sub(fq2_sub(ZS, Z1Z1), Z2Z2), H);
   r = r16_run(R, gl);
-  const fq2 I = r16_get_sqr(r, 0, gbase), RR = r16_get_sqr(r, 2, gbase), Z3 = r16_get_mul(r, 4, gbase);
+  const fq2 I = r16_get_sqr<0>(r), RR = r16_get_sqr<2>(r), Z3 = r16_get_mul<4>(r);
   // round 4: J = H I, V = U1 I
   r16_mul(R, 0, H, I);
   r16_mul(R, 4, U1, I);
   r = r16_run(R, gl);
-  const fq2 J = r16_get_mul(r, 0, gbase), V = r16_get_mul(r, 4, gbase);
+  const fq2 J = r16_get_mul<0>(r), V = r16_get_mul<4>(r);
   const fq2 X3 = fq2_sub(fq2_sub(RR, J), fq2_dbl(V));
   // round 5: r (V - X3), S1 J
   r16_mul(R, 0, rr, fq2_sub(V, X3));
   r16_mul(R, 4, S1, J);
   r = r16_run(R, gl);
-  const fq2 Y3 = fq2_sub(r16_get_mul(r, 0, gbase), fq2_dbl(r16_get_mul(r, 4, gbase)));
+  const fq2 Y3 = fq2_sub(r16_get_mul<0>(r), fq2_dbl(r16_get_mul<4>(r)));
   return g2j{X3, Y3, Z3};
 }
 __device__ __forceinline__ g2j g2_sub_group(const g2j& p, const g2j& q, int gl, int gbase) {
@@ -507,6 +519,9 @@ __device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
 // clearing.  A cleared point equal to the identity makes the sequential loop continue with the next
 // candidate; so does this one (base = winner + 1).  `active` must be group-uniform.
 // Returns true on the lane that holds the result in `out`.
+#ifndef HBX_PHASE
+#define HBX_PHASE(k)  // profiling hook (tools/microbench/hashg2.hip records wall-clock stamps)
+#endif
 template <int K>
 __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
   static_assert(K >= 8 && K <= 32 && (64 % K) == 0, "group size (the cofactor clearing uses 8 lanes)");
@@ -529,6 +544,7 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
       greatest = (chacha_next_u32(r) & 1u) != 0;
       drawn++;
     }
+    HBX_PHASE(1);
     const fq2 rhs = fq2_add(fq2_mul(fq2_sqr(x), x), g2_b());
     const bool c1zero = fq_is_zero(rhs.c1);
     fq s = fq_zero();
@@ -536,6 +552,7 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
     bool sq;
     if (c1zero) sq = fq2_sqrt(rhs, y0);  // measure-zero branch, exact general square root
     else sq = fq2_norm_sqrt(rhs, s);
+    HBX_PHASE(2);
     const uint64_t pass = __ballot(sq) & gmask;
     if (pass == 0) {
       base += K;
@@ -548,11 +565,13 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
       // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
       if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
     }
+    HBX_PHASE(3);
     // the winner's point to every lane of the group, then the cooperative cofactor clearing
     const int src = gbase + win;
     const fq2 xw = fq2{fq_from_lane(x.c0, src), fq_from_lane(x.c1, src)};
     const fq2 yw = fq2{fq_from_lane(y.c0, src), fq_from_lane(y.c1, src)};
     out = g2_clear_cofactor_group(g2j{xw, yw, fq2_one()}, gl, gbase);
+    HBX_PHASE(4);
     const bool ident = g2j_is_identity(out);
     if ((__ballot(ident) & gmask) == 0) return gl == win;
     base += (uint32_t)win + 1;

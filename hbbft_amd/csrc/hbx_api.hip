@@ -86,8 +86,7 @@ struct hbx_ctx {
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
-      coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96,
-      coin_comb_lines, coin_comb_c2;
+      coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
@@ -430,7 +429,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96, &c->coin_comb_lines, &c->coin_comb_c2, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
+                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -906,9 +905,7 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   const uint32_t I = c->coin_I;
   if (!c->coin_comb.ensure((size_t)I * sizeof(g2a)) || !c->coin_comb_st.ensure((size_t)I * 4) ||
       !c->coin_mpk_comp.ensure(48) || !c->coin_mpk.ensure(sizeof(g1a)) || !c->coin_mpk_st.ensure(4) ||
-      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96) ||
-      !c->coin_comb_lines.ensure((size_t)I * MILLER_LINES * sizeof(line_pre)) ||
-      !c->coin_comb_c2.ensure((size_t)I * MILLER_LINES * sizeof(fq2)))
+      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_signatures: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, s, c->coin_mpk_comp.as<uint8_t>(), 1u, c->coin_mpk.as<g1a>(),
@@ -919,29 +916,13 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   HIPCHK(c, hipStreamSynchronize(s));
   if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
   {
+    // the G2 combine (blocks y = 0) and the master-key check (y = 1) in one launch
     timed t_(c, HBX_K_COMBINE_SIGS, s);
-    hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
-                       c->coin_sig.as<g2a>(), c->coin_n, t, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>());
+    hipLaunchKernelGGL(k_combine_sigs, dim3(I, 2), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
+                       c->coin_sig.as<g2a>(), c->coin_n, t, c->pk.as<g1a>(), c->coin_mpk.as<g1a>(),
+                       c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());
-  // lines of the combined signatures (16-lane groups, then one lane per line for the
-  // normalisation), the master checks three lanes each, parity and encoding
-  {
-    timed t_(c, HBX_K_MASTER_VERIFY, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((I * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(), I,
-                       c->coin_comb_lines.as<line_pre>(), c->coin_comb_c2.as<fq2>(), nullptr, 0u, nullptr, nullptr,
-                       nullptr);
-    HIPCHK(c, hipGetLastError());
-    const uint32_t nl = I * MILLER_LINES;
-    hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_comb_lines.as<line_pre>(),
-                       c->coin_comb_c2.as<fq2>(), nl);
-    HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(k_master_verify3, dim3((I + G3_PER_WAVE - 1) / G3_PER_WAVE), dim3(64), 0, s,
-                       c->coin_lines.as<line_pre>(), c->coin_H.as<g2a>(), c->coin_mpk.as<g1a>(),
-                       c->coin_comb_lines.as<line_pre>(), c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), I,
-                       c->coin_ok.as<uint8_t>());
-    HIPCHK(c, hipGetLastError());
-  }
   hipLaunchKernelGGL(k_sig_parity, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(),
                      c->coin_comb_st.as<int32_t>(), I, c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
   HIPCHK(c, hipGetLastError());

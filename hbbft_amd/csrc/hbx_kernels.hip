@@ -141,7 +141,7 @@ constexpr int LINE_K = 16;
 // line_dbl_step (pairing.hpp) on the LINE_K lanes of a group that all hold T: its 26 Fq
 // products as three rounds of independent products, one per lane (10, 14 and 8 lanes busy),
 // exchanged by ds_bpermute; Fq2 products by schoolbook.  Same values mod p as line_dbl_step.
-__device__ __noinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& c2, int gl, int gbase) {
+__device__ __forceinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& c2, int gl, int gbase) {
   const fq x0 = T.x.c0, x1 = T.x.c1, y0 = T.y.c0, y1 = T.y.c1, z0 = T.z.c0, z1 = T.z.c1;
   // round 1: A = X^2 (0, 1), B = Y^2 (2, 3), ZZ = Z^2 (4, 5), Y Z (6..9)
   fq r;
@@ -150,13 +150,13 @@ __device__ __noinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& 
                       x0, x0, x0, x0, x0, x0};
     const fq b[16] = {fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, fq_sub(z0, z1), z1, z0, z1, z1, z0,
                       x1, x1, x1, x1, x1, x1};
-    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
   }
-  const fq2 A = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
-  const fq2 B = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
-  const fq2 ZZ = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
-  const fq2 YZ = fq2{fq_sub(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7)),
-                     fq_add(fq_from_lane(r, gbase + 8), fq_from_lane(r, gbase + 9))};
+  const fq2 A = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
+  const fq2 B = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
+  const fq2 ZZ = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
+  const fq2 YZ = fq2{fq_sub(fq_from_row<6>(r), fq_from_row<7>(r)),
+                     fq_add(fq_from_row<8>(r), fq_from_row<9>(r))};
   // round 2: C = B^2 (0, 1), (X + B)^2 (2, 3), F = E^2 (4, 5), E X (6..9), E ZZ (10..13)
   const fq2 E = fq2_add(fq2_dbl(A), A);
   const fq2 S = fq2_add(T.x, B);
@@ -165,15 +165,15 @@ __device__ __noinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& 
                       E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c0};
     const fq b[16] = {fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1,
                       x0, x1, x1, x0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0, E.c1, E.c1};
-    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
   }
-  const fq2 C = fq2{fq_from_lane(r, gbase + 0), fq_dbl(fq_from_lane(r, gbase + 1))};
-  const fq2 TT = fq2{fq_from_lane(r, gbase + 2), fq_dbl(fq_from_lane(r, gbase + 3))};
-  const fq2 F = fq2{fq_from_lane(r, gbase + 4), fq_dbl(fq_from_lane(r, gbase + 5))};
-  const fq2 EX = fq2{fq_sub(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7)),
-                     fq_add(fq_from_lane(r, gbase + 8), fq_from_lane(r, gbase + 9))};
-  const fq2 EZZ = fq2{fq_sub(fq_from_lane(r, gbase + 10), fq_from_lane(r, gbase + 11)),
-                      fq_add(fq_from_lane(r, gbase + 12), fq_from_lane(r, gbase + 13))};
+  const fq2 C = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
+  const fq2 TT = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
+  const fq2 F = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
+  const fq2 EX = fq2{fq_sub(fq_from_row<6>(r), fq_from_row<7>(r)),
+                     fq_add(fq_from_row<8>(r), fq_from_row<9>(r))};
+  const fq2 EZZ = fq2{fq_sub(fq_from_row<10>(r), fq_from_row<11>(r)),
+                      fq_add(fq_from_row<12>(r), fq_from_row<13>(r))};
   c0 = fq2_sub(EX, fq2_dbl(B));
   c1 = fq2_neg(EZZ);
   const fq2 D = fq2_dbl(fq2_sub(fq2_sub(TT, A), C));
@@ -186,12 +186,12 @@ __device__ __noinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& 
                       E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0};
     const fq b[16] = {G.c0, G.c1, G.c1, G.c0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0,
                       G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0};
-    r = fq_mul(fq_sel16(gl, a), fq_sel16(gl, b));
+    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
   }
-  const fq2 EG = fq2{fq_sub(fq_from_lane(r, gbase + 0), fq_from_lane(r, gbase + 1)),
-                     fq_add(fq_from_lane(r, gbase + 2), fq_from_lane(r, gbase + 3))};
-  c2 = fq2{fq_sub(fq_from_lane(r, gbase + 4), fq_from_lane(r, gbase + 5)),
-           fq_add(fq_from_lane(r, gbase + 6), fq_from_lane(r, gbase + 7))};
+  const fq2 EG = fq2{fq_sub(fq_from_row<0>(r), fq_from_row<1>(r)),
+                     fq_add(fq_from_row<2>(r), fq_from_row<3>(r))};
+  c2 = fq2{fq_sub(fq_from_row<4>(r), fq_from_row<5>(r)),
+           fq_add(fq_from_row<6>(r), fq_from_row<7>(r))};
   const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
   T = g2j{X3, fq2_sub(EG, C8), Z3};
 }
@@ -808,16 +808,32 @@ __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
 // lambda_k = d0 + d1 X + d2 X^2 + d3 X^3 (|d_i| < X < 2^64),
 //     lambda_k S_k = d0 S_k - d1 psi(S_k) + d2 psi^2(S_k) - d3 psi^3(S_k),
 // four independent 64-bit scalar multiplications, one per lane (lane 4k + i), instead of one
-// 255-bit multiplication: a quarter of the doubling chain.  One block per instance.
+// 255-bit multiplication: a quarter of the doubling chain.
+//
+// B3 master check (PublicKey::verify(sig, nonce), common_coin.rs:196) in the same launch, on
+// blocks y = 1: every S_k was verified, e(pk_k, H) = e(g1, S_k), so by bilinearity
+//     e(g1, sig) = prod e(g1, S_k)^lambda_k = e(sum lambda_k pk_k, H),
+// and e(master_pk, H) = e(g1, sig)  <=>  sum lambda_k pk_k = master_pk  (H != O, prime order):
+// the same bit as the pairing check, from a G1 Lagrange sum over the same index set (GLV halves
+// on two lanes, 4-bit windows, like k_combine) -- concurrent with the G2 sum instead of a pairing
+// after it.  master_ok = 0 where the combine fails.  One block per (instance, part).
 // status: 0 or -3 (NotEnoughShares).
 constexpr int SIGCOMB_THREADS = 256;
+__device__ __forceinline__ g1j g1j_shfl_xor(const g1j& a, int m) {
+  return g1j{fq_shfl_xor(a.x, m), fq_shfl_xor(a.y, m), fq_shfl_xor(a.z, m)};
+}
 __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t* __restrict__ valid,
                                                                   const g2a* __restrict__ sig, uint32_t n, uint32_t t,
-                                                                  g2a* __restrict__ out, int32_t* __restrict__ status) {
+                                                                  const g1a* __restrict__ pk,
+                                                                  const g1a* __restrict__ master_pk,
+                                                                  g2a* __restrict__ out, int32_t* __restrict__ status,
+                                                                  uint8_t* __restrict__ master_ok) {
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;
-  __shared__ g2j red[SIGCOMB_THREADS / 64];
+  __shared__ g2j red2[SIGCOMB_THREADS / 64];
+  __shared__ g1j red1[SIGCOMB_THREADS / 64];
   const uint32_t inst = blockIdx.x;
+  const bool g1_part = blockIdx.y == 1;
   const int tid = threadIdx.x;
   if (tid == 0) {
     int c = 0;
@@ -828,8 +844,41 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
   __syncthreads();
   if (s_count < (int)t) {
     if (tid == 0) {
-      status[inst] = -3;
-      out[inst].inf = true;
+      if (g1_part) {
+        master_ok[inst] = 0;
+      } else {
+        status[inst] = -3;
+        out[inst].inf = true;
+      }
+    }
+    return;
+  }
+  if (g1_part) {
+    g1j acc = g1_identity();
+    for (int q = tid; q < 2 * (int)t; q += SIGCOMB_THREADS) {
+      const int k = q >> 1;
+      const fr lam = lagrange_at_zero(idx, (int)t, k);
+      uint32_t k1[4], k2[4];
+      g1_glv_split(lam.l, k1, k2);
+      g1a pp = pk[idx[k]];
+      if (q & 1) pp.x = fq_mul(pp.x, fq_from_const(G1_BETA));
+      acc = g1_add(acc, g1_mul_u128_w4(pp, (q & 1) ? k2 : k1));
+    }
+#pragma unroll 1
+    for (int m = 1; m < 64; m <<= 1) acc = g1_add(acc, g1j_shfl_xor(acc, m));
+    if ((tid & 63) == 0) red1[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      g1j sum = red1[0];
+      for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g1_add(sum, red1[w]);
+      // sum == master_pk (affine, not the identity): X = x Z^2, Y = y Z^3
+      const g1a M = master_pk[0];
+      bool eq = !g1j_is_identity(sum) && !M.inf;
+      if (eq) {
+        const fq zz = fq_sqr(sum.z);
+        eq = fq_eq(sum.x, fq_mul(M.x, zz)) && fq_eq(sum.y, fq_mul(M.y, fq_mul(zz, sum.z)));
+      }
+      master_ok[inst] = eq ? 1 : 0;
     }
     return;
   }
@@ -846,38 +895,14 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
   }
 #pragma unroll 1
   for (int m = 1; m < 64; m <<= 1) acc = g2_add(acc, g2j_shfl_xor(acc, m));
-  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  if ((tid & 63) == 0) red2[tid >> 6] = acc;
   __syncthreads();
   if (tid == 0) {
-    g2j sum = red[0];
-    for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g2_add(sum, red[w]);
+    g2j sum = red2[0];
+    for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g2_add(sum, red2[w]);
     out[inst] = g2_to_affine(sum);
     status[inst] = 0;
   }
-}
-
-// B3 master check (PublicKey::verify, common_coin.rs:196): e(master_pk, H_j) e(-g1, sig_j) == 1
-// with prepared lines for both G2 points (H_j from hbx_prepare_nonces, sig_j by k_prepare_lines),
-// three lanes per check (pairing3.hpp).  Instances whose combine failed get master_ok = 0.
-__global__ void __launch_bounds__(64) k_master_verify3(const line_pre* __restrict__ h_lines, const g2a* __restrict__ H,
-                                                       const g1a* __restrict__ master_pk,
-                                                       const line_pre* __restrict__ sig_lines, const g2a* __restrict__ sig,
-                                                       const int32_t* __restrict__ status, uint32_t count,
-                                                       uint8_t* __restrict__ master_ok) {
-  const int lane = (int)(threadIdx.x & 63);
-  const grp3 g = grp3_of_lane();
-  const uint32_t j = blockIdx.x * G3_PER_WAVE + (uint32_t)(lane / G3);
-  if (lane == 63 || j >= count) return;  // whole groups
-  bool ok = false;
-  if (status[j] == 0) {
-    g1a ng;
-    ng.x = fq_from_const(G1_GEN_X);
-    ng.y = fq_neg(fq_from_const(G1_GEN_Y));
-    ng.inf = false;
-    ok = check2_g3<false>(h_lines + (size_t)j * MILLER_LINES, master_pk[0], H[j].inf,
-                          sig_lines + (size_t)j * MILLER_LINES, ng, sig[j].inf, g);
-  }
-  if (g.gl == 0) master_ok[j] = ok ? 1 : 0;
 }
 
 // B4 Signature::parity (common_coin.rs:173) and the compressed signature, one lane per instance.

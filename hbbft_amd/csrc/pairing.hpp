@@ -124,16 +124,17 @@ HBX_HDNI fq12 mul_by_line(const fq12& f, const line_pre& l, const g1a& P) {
 // for x < 0.  PA / PB are affine; a pair whose `use` flag is false contributes 1 (a pairing
 // with the identity).
 // Inlined into its kernel with ONE copy each of the Fq12 squaring and the sparse line product
-// (the line loop is not unrolled): f stays in registers instead of crossing call boundaries
-// through scratch (an out-of-line Fq12 argument/result is a 576-byte scratch round trip), and
-// the line addresses stay wave-uniform (kernel argument + block index + loop counters).
+// (the line loop is not unrolled), Fq products inlined too (FqInl): f stays in registers instead
+// of crossing call boundaries through scratch (an out-of-line Fq12 argument/result is a 576-byte
+// scratch round trip), and the line addresses stay wave-uniform (kernel argument + block index +
+// loop counters).
 HBX_HD fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const line_pre* LB,
                          const g1a& PB, bool useB) {
   fq12 f = fq12_one();
   int k = 0;
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    if (i != 62) f = fq12_sqr_i(f);
+    if (i != 62) f = fq12_sqr_t<FqInl>(f);
     const int steps = ((BLS_X >> i) & 1) ? 4 : 2;  // (A, B) lines of the doubling [+ addition]
 #pragma unroll 1
     for (int s = 0; s < steps; s++) {
@@ -142,7 +143,7 @@ HBX_HD fq12 miller_loop2(const line_pre* LA, const g1a& PA, bool useA, const lin
       if (b ? useB : useA) {
         const fq px = b ? PB.x : PA.x;
         const fq py = b ? PB.y : PA.y;
-        f = fq12_mul_by_014_i(f, L.c0, fq2_mul_fq(L.c1, px), py);
+        f = fq12_mul_by_014_t<FqInl>(f, L.c0, fq2_mul_fq_t<FqInl>(L.c1, px), py);
       }
       if (b) k++;
     }
@@ -248,10 +249,10 @@ __device__ __forceinline__ fq12 lds_get_fq12(const lds_u32* base) {
   for (int i = 0; i < 144; i++) p[i] = base[i * LDS_FQ12_STRIDE];
   return a;
 }
-// r^(2^k) by k cyclotomic squarings: only r is live in the loop
+// r^(2^k) by k cyclotomic squarings (Fq products inlined): only r is live in the loop
 __device__ __forceinline__ fq12 cyc_sqr_n(fq12 r, int k) {
 #pragma unroll 1
-  for (int i = 0; i < k; i++) r = fq12_cyclotomic_sqr_i(r);
+  for (int i = 0; i < k; i++) r = fq12_cyclotomic_sqr_t<FqInl>(r);
   return r;
 }
 // g^|x| with |x| = 0xd201000000010000 written out as runs of squarings between its one bits
@@ -260,17 +261,16 @@ __device__ __forceinline__ fq12 cyc_sqr_n(fq12 r, int k) {
 __device__ __noinline__ fq12 cyc_exp_abs_x_lds(const fq12& g_in, lds_u32* gslot) {
   static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
   lds_put_fq12(gslot, g_in);
-  fq12 r = cyc_sqr_n(g_in, 1);  // bit 62
-  r = fq12_mul(r, lds_get_fq12(gslot));
-  r = cyc_sqr_n(r, 2);          // bit 60
-  r = fq12_mul(r, lds_get_fq12(gslot));
-  r = cyc_sqr_n(r, 3);          // bit 57
-  r = fq12_mul(r, lds_get_fq12(gslot));
-  r = cyc_sqr_n(r, 9);          // bit 48
-  r = fq12_mul(r, lds_get_fq12(gslot));
-  r = cyc_sqr_n(r, 32);         // bit 16
-  r = fq12_mul(r, lds_get_fq12(gslot));
-  return cyc_sqr_n(r, 16);      // bits 15..0
+  // squaring runs before the multiplications at bits 62, 60, 57, 48, 16, then bits 15..0; one
+  // copy of the (inlined) squaring loop
+  fq12 r = g_in;
+#pragma unroll 1
+  for (int q = 0; q < 6; q++) {
+    const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
+    r = cyc_sqr_n(r, run);
+    if (q < 5) r = fq12_mul(r, lds_get_fq12(gslot));
+  }
+  return r;
 }
 __device__ __forceinline__ fq12 cyc_exp_x_lds(const fq12& g, lds_u32* gslot) {
   return fq12_conj(cyc_exp_abs_x_lds(g, gslot));

@@ -115,12 +115,11 @@ const char* hbx_version(void);
 #define HBX_K_VERIFY_SHARES 3   /* decryption-share pairing checks */
 #define HBX_K_COMBINE 4         /* Lagrange combine + key derivation per proposer */
 #define HBX_K_VERIFY_SIG 5      /* coin signature-share checks */
-#define HBX_K_COMBINE_SIGS 6    /* coin G2 Lagrange combine */
+#define HBX_K_COMBINE_SIGS 6    /* coin G2 Lagrange combine + master-key check */
 #define HBX_K_RS_CODE 7         /* Reed-Solomon encode / reconstruct passes */
 #define HBX_K_MERKLE_LEAVES 8   /* SHA-256 leaf hashes */
 #define HBX_K_HASH_NONCES 9     /* coin nonce hash_g2 */
-#define HBX_K_MASTER_VERIFY 10  /* coin: lines of the combined signatures + master-key checks */
-#define HBX_K_COUNT 11
+#define HBX_K_COUNT 10
 int hbx_set_timing(hbx_ctx* ctx, int on);
 int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launches);
 

@@ -61,7 +61,7 @@ def coin(ctx, steps):
         times["verify_sig_shares"].append(t2 - t1)
         times["combine_signatures"].append(t3 - t2)
     kern = {}
-    for name in ("hash_nonces", "verify_sig", "combine_sigs", "master_verify"):
+    for name in ("hash_nonces", "verify_sig", "combine_sigs"):
         ms_, cnt_ = ctx.kernel_time(name)
         kern[name] = round(ms_ / max(cnt_, 1), 3)
     k_ms, k_cnt = ctx.kernel_time("verify_sig")

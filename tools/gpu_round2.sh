@@ -10,5 +10,12 @@ timeout -k 10 300 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_ou
 cat gpurun_out/${tag}_bench.json
 timeout -k 10 200 python -u bench.py --shard-of 8 --no-cpu-baseline > gpurun_out/${tag}_bench_shard8.json 2> gpurun_out/${tag}_bench_shard8.err || { echo "shard8 failed"; exit 1; }
 cat gpurun_out/${tag}_bench_shard8.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o prof -- python3 bench.py --steps 3 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_prof -o prof -- python3 bench.py --steps 3 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/${tag}_prof.log; exit 1; }
 echo done
+timeout -k 10 300 python -u tools/bench_aux.py > gpurun_out/${tag}_aux.jsonl 2> gpurun_out/${tag}_aux.err || { echo "aux failed"; tail -20 gpurun_out/${tag}_aux.err; exit 1; }
+cat gpurun_out/${tag}_aux.jsonl
+for b in tools/microbench/hashg2 tools/microbench/parts tools/microbench/parts_w2; do
+  [ -x "$b" ] || continue
+  echo "== $b"; timeout -k 10 120 ./$b > gpurun_out/${tag}_$(basename $b).txt 2>&1 || { echo "$b failed"; cat gpurun_out/${tag}_$(basename $b).txt; exit 1; }
+  cat gpurun_out/${tag}_$(basename $b).txt
+done

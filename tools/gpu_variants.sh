@@ -13,7 +13,7 @@ timeout -k 10 300 python -u tools/bench_aux.py --only c4 > gpurun_out/${tag}_c4.
 cat gpurun_out/${tag}_c4.json
 for lib in hbbft_amd/libhbx*.so; do
   v=$(basename $lib .so)
-  for mode in "--shard-of 8" "" "--verify-lanes 3"; do
+  for mode in "--shard-of 8" ""; do
     HBX_LIB_PATH=$PWD/$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 3 $mode > gpurun_out/${tag}_run.json 2> gpurun_out/${tag}_run.err || { echo "$v $mode failed"; tail -5 gpurun_out/${tag}_run.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open('gpurun_out/${tag}_run.json')); print('$v', '$mode', d['ms_per_step'], d['kernels_ms'])" | tee -a gpurun_out/${tag}_summary.txt
   done

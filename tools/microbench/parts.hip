@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "../../hbbft_amd/csrc/pairing.hpp"
+#ifndef PARTS_WAVES
+#define PARTS_WAVES 1
+#endif
 
 using namespace hbx;
 
@@ -15,14 +18,14 @@ __device__ fq seed_fq(uint32_t s) {
   return a;
 }
 
-__global__ void __launch_bounds__(64) k_miller(const line_pre* lines, uint32_t* out) {
+__global__ void __launch_bounds__(64, PARTS_WAVES) k_miller(const line_pre* lines, uint32_t* out) {
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
   g1a P{seed_fq(t), seed_fq(t + 7), false}, Q{seed_fq(t + 3), seed_fq(t + 9), false};
   const fq12 f = miller_loop2(lines, P, true, lines + MILLER_LINES, Q, true);
   out[t] = f.c0.c0.c0.l[0] ^ f.c1.c2.c1.l[11];
 }
 
-__global__ void __launch_bounds__(64) k_finalexp(uint32_t* out) {
+__global__ void __launch_bounds__(64, PARTS_WAVES) k_finalexp(uint32_t* out) {
   __shared__ uint32_t gslots[144 * LDS_FQ12_STRIDE];
   const uint32_t t = blockIdx.x * 64 + threadIdx.x;
   fq12 f;
