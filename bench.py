@@ -52,14 +52,15 @@ MADS_PER_FQMUL = 288
 # tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
-# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_pmc4.sh,
-# profiles/r01_s6_pmc_n256.txt): 3.232e6 KB + 6.434e6 KB per launch.  The accesses are the
-# kernel's scratch spills (dword / dwordx4 scratch_load/store of the Fq12 state around the
-# out-of-line Fq product), a width the guide leaves uncalibrated, so the raw counter bytes are
-# reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~10 MB
-# (shares 48 B + pk + 26 KB of lines per proposer + 1 B out): the kernel is VALU-bound, and this
-# traffic (~0.32 TB/s at 30.7 ms) is spill re-reads, not data movement the algorithm needs.
-TRAFFIC_N256_BYTES = (3.232e6 + 6.434e6) * 1024
+# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_r02d.sh,
+# profiles/r02d_pmc_hbm_bytes.txt, measured on the round-2 kernel): 3.784e6 KB + 7.062e6 KB per
+# launch.  The accesses are the kernel's scratch traffic at the out-of-line Fq12 calls of the
+# final exponentiation (fq12 operands and results pass through the stack), a width the guide
+# leaves uncalibrated, so the raw counter bytes are reported without the x2 streaming-read
+# correction.  Algorithmic bytes per launch are ~10 MB (shares 48 B + pk + 26 KB of lines per
+# proposer + 1 B out): the kernel is VALU-bound and the traffic (~0.38 TB/s) is not its bound.
+TRAFFIC_N256_BYTES = (3.784e6 + 7.062e6) * 1024
+TRAFFIC_SOURCE = "profiles/r02d_pmc_hbm_bytes.txt (PMC FETCH_SIZE+WRITE_SIZE, round-2 kernel)"
 # The benchmarked node is validator 0: its own decryption shares are computed locally
 # (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
 OWN_INDEX = 0
@@ -352,7 +353,7 @@ def main():
         "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
                      "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4),
                      "traffic": TRAFFIC_N256_BYTES if (n == 256 and pj == 256) else None,
-                     "traffic_note": "bytes/launch, PMC FETCH_SIZE+WRITE_SIZE (scratch spills); algorithmic ~1e7",
+                     "traffic_note": "bytes/launch from " + TRAFFIC_SOURCE + " (scratch at Fq12 calls); algorithmic ~1e7",
                      "kernel": "k_verify_shares", "kernel_ms": ms_kernel,
                      "work": f"{shares_here} shares x {FQMUL_PER_SHARE_VERIFY} Fq-mul x {MADS_PER_FQMUL} MAD"},
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
