@@ -15,7 +15,7 @@ dependency ``pairing = 0.14.2`` (reference ``Cargo.toml:28``) that hbbft's hot p
   0.14 schedules its line functions.
 
 Parity status: pinned by the BLS12-381 known answers of SURVEY.md App. A.2 (generator encodings,
-r, cofactors), checked in ``tests/test_oracle_bls.py``, plus algebraic identities (bilinearity,
+r, cofactors), checked in ``tests/test_oracle_kat.py``, plus algebraic identities (bilinearity,
 e^r = 1, subgroup orders).  The reference crates are not present in this container, so nothing
 here was compared byte-for-byte against pairing 0.14 itself.
 

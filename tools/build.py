@@ -37,19 +37,6 @@ def build_hbx(force=False):
     return out
 
 
-def build_oracle(force=False):
-    src = os.path.join(ROOT, "oracle", "bls_cpu.c")
-    if not os.path.exists(src):
-        return None
-    outdir = os.path.join(ROOT, "oracle", "_build")
-    os.makedirs(outdir, exist_ok=True)
-    out = os.path.join(outdir, "liboracle_bls.so")
-    if not force and newer(out, [src]):
-        return out
-    run(["gcc", "-O3", "-march=x86-64-v3", "-std=c11", "-shared", "-fPIC", "-pthread", "-o", out, src])
-    return out
-
-
 def build_cpu_port(force=False):
     """CPU baseline (bench.py cpu_baseline leg only): the reference's per-share algorithm shape."""
     src = os.path.join(ROOT, "tools", "cpu_baseline", "cpu_port.cpp")
@@ -66,5 +53,4 @@ def build_cpu_port(force=False):
 if __name__ == "__main__":
     force = "--force" in sys.argv
     build_hbx(force)
-    build_oracle(force)
     build_cpu_port(force)
