@@ -9,6 +9,9 @@
 // column) and the integer VALU for SHA-256 (64 rounds per 64-byte block); no MFMA.
 #pragma once
 #include "hash.hpp"
+#ifndef HBX_IN_TU
+#define HBX_IN_TU(n) 1  // single-TU build (hbx_kernels.hip defines the split)
+#endif
 
 namespace hbx {
 
@@ -47,6 +50,7 @@ struct rs_job {
 // grid (ceil(L / (4 * 256)), inst); thread = 4 consecutive byte columns of one instance.
 // coef: [inst][RS_MAX_N][k] logs (GF_COEF_ZERO for 0).  Coefficient reads are wave-uniform.
 // job_stride = 0: every instance runs job 0 (encode); 1: per-instance jobs (reconstruct).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(256) k_rs_code(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
                                                  uint32_t k, const rs_job* __restrict__ jobs,
                                                  const uint16_t* __restrict__ coef, uint32_t job_stride,
@@ -100,6 +104,7 @@ __global__ void __launch_bounds__(256) k_rs_code(uint8_t* __restrict__ shards, s
     }
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // GF(2^8) coding by byte permutes.  Multiplication by a fixed coefficient c is GF(2)-linear, so
@@ -119,6 +124,7 @@ struct alignas(32) gf_ptab {
 
 // Perm tables for per-instance jobs (reconstruct): one lane per coefficient of jobs[inst]
 // (logs in coef, GF_COEF_ZERO = 0).  grid (ceil(RS_MAX_N * k / 256), inst).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(256) k_rs_perm_tables(const rs_job* __restrict__ jobs, const uint16_t* __restrict__ coef,
                                                         uint32_t k, const uint16_t* __restrict__ glog,
                                                         const uint8_t* __restrict__ gexp, gf_ptab* __restrict__ tables) {
@@ -143,6 +149,7 @@ __global__ void __launch_bounds__(256) k_rs_perm_tables(const rs_job* __restrict
   t.w[5] = t.w[6] = t.w[7] = 0;
   tables[(size_t)inst * RS_MAX_N * k + e] = t;
 }
+#endif
 
 // 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -161,6 +168,7 @@ __host__ __device__ constexpr size_t rs_perm_lds_bytes(uint32_t k, int ch) {
   return (size_t)((k + 1) & ~1u) * ch * 20;
 }
 
+#if HBX_IN_TU(6)
 template <int CH, int D>
 __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
                                                       uint32_t k, const rs_job* __restrict__ jobs,
@@ -254,11 +262,25 @@ __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shar
     }
   }
 }
+#endif
+#if defined(HBX_TU) && HBX_TU == 6
+// the tiles rs_code() (hbx_api.hip) launches, instantiated in this translation unit
+#define HBX_RS_INST(ch, d)                                                                                   \
+  template __global__ void k_rs_code_perm<ch, d>(uint8_t* __restrict__, size_t, uint32_t, uint32_t,            \
+                                                  const rs_job* __restrict__, const gf_ptab* __restrict__, uint32_t);
+HBX_RS_INST(32, 2)
+HBX_RS_INST(32, 4)
+HBX_RS_INST(64, 2)
+HBX_RS_INST(24, 4)
+HBX_RS_INST(48, 2)
+#undef HBX_RS_INST
+#endif
 
 // reconstruct_shards set-up, one block per instance (reed-solomon-erasure 3.1.0):
 // first k present shards -> invert that k x k sub-matrix of the encoding matrix (Gauss-Jordan in
 // LDS) -> job 0: rebuild missing data shards from the k sub shards; job 1: re-encode missing
 // parity shards from the (then complete) data shards.  status: 0, or HBX_E_TOO_FEW_SHARDS.
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __restrict__ present, uint32_t k,
                                                               uint32_t m, const uint8_t* __restrict__ enc,
                                                               const uint16_t* __restrict__ glog,
@@ -367,6 +389,7 @@ __global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __r
     cp[o * k + c] = v ? T.lg[v] : GF_COEF_ZERO;
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // SHA-256 of (prefix bytes) || data[len]: one lane per message; the bulk of the data is read as
@@ -529,6 +552,7 @@ __device__ __forceinline__ void merkle_node(int variant, const uint32_t* l8, con
 
 // Leaf hashes of the index-prefixed shards: leaf(i) = H_leaf([i] || shard_i).
 // grid (ceil(n/64), inst); out: u32[inst][n][8] (digest words, big-endian order).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict__ shards, size_t inst_stride,
                                                       uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
                                                       int variant) {
@@ -541,6 +565,7 @@ __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict_
 #pragma unroll
   for (int q = 0; q < 8; q++) o[q] = h[q];
 }
+#endif
 
 // SHA-256 Merkle leaves (HBX_MERKLE_SHA256), two waves per 64 leaves of one instance:
 //  * wave 1 (producer) loads each leaf's next 64-byte block, expands the message schedule and
@@ -555,6 +580,7 @@ __device__ __forceinline__ uint32_t sha_sig(uint32_t x, int r1, int r2, int r3) 
   return xor3(rotr32(x, r1), rotr32(x, r2), rotr32(x, r3));
 }
 
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __restrict__ shards, size_t inst_stride,
                                                               uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash) {
   __shared__ uint4 kw[2][16][64];  // [slot][rounds / 4][lane]
@@ -657,6 +683,7 @@ __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __r
     for (int q = 0; q < 8; q++) o[q] = H[q];
   }
 }
+#endif
 
 // Number of stored tree nodes for n leaves: every level from the leaves (n) to the root (1),
 // with a promoted odd node stored again on the level it moves to.
@@ -674,6 +701,7 @@ __host__ __device__ inline uint32_t merkle_node_count(uint32_t n) {
 // instance, the level in LDS.  roots: u8[inst][32]; nodes (optional): u8[inst][node_count][32],
 // level-major from the leaf level up, the root last (the `(2n - 1) x 32` tree of SURVEY.md
 // §8(b) hbx_merkle_build, plus the promoted copies).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(128) k_merkle_tree(const uint32_t* __restrict__ leaf_hash, uint32_t n,
                                                      uint8_t* __restrict__ roots, uint8_t* __restrict__ nodes,
                                                      int variant) {
@@ -713,6 +741,7 @@ __global__ void __launch_bounds__(128) k_merkle_tree(const uint32_t* __restrict_
     roots[(size_t)inst * 32 + threadIdx.x] = (uint8_t)(wv >> (8 * (3 - threadIdx.x % 4)));
   }
 }
+#endif
 
 // MerkleTree::gen_proof (broadcast.rs:389-401 asks one per node) from the stored tree: proof q
 // is for leaf req[2q + 1] of instance req[2q]; like merkle.rs it is the proof of the FIRST leaf
@@ -720,6 +749,7 @@ __global__ void __launch_bounds__(128) k_merkle_tree(const uint32_t* __restrict_
 // broadcast.rs:371-372, but the semantics are kept).  Output in the layout k_merkle_validate
 // reads: node path root first ... leaf digest (depth + 1 entries of 32 B), the sibling of each
 // lemma level, `sides` bit l = the level-l sibling is Positioned::Left, depth, root.
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(64) k_merkle_proofs(const uint8_t* __restrict__ nodes, uint32_t n,
                                                       const uint32_t* __restrict__ req, uint32_t count,
                                                       uint8_t* __restrict__ node_hash, uint8_t* __restrict__ sib_hash,
@@ -773,6 +803,7 @@ __global__ void __launch_bounds__(64) k_merkle_proofs(const uint8_t* __restrict_
   sides[q] = side_out;
   depth[q] = d;
 }
+#endif
 
 // Broadcast::validate_proof (broadcast.rs:555-575) over a batch of proofs:
 //   Proof::validate(root): root == lemma[0].node_hash == the proof's root_hash, every
@@ -781,6 +812,7 @@ __global__ void __launch_bounds__(64) k_merkle_proofs(const uint8_t* __restrict_
 // Per proof j: value = values + j * vlen (the index byte first), depth[j] <= 16,
 // nodes = node_hash + j * 17 * 32 (root first, leaf hash last), sibs = sib_hash + j * 16 * 32,
 // sides bit k set = sibling at level k is on the LEFT (merkle.rs Positioned::Left).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restrict__ values, uint32_t vlen,
                                                         const uint8_t* __restrict__ node_hash,
                                                         const uint8_t* __restrict__ sib_hash,
@@ -829,11 +861,13 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
   ok = ok && val[0] == sender[j] && idx == val[0];
   valid[j] = ok ? 1 : 0;
 }
+#endif
 
 // glue_shards (broadcast.rs:697-707): the payload is bytes [4, 4 + len) of the first k shards
 // (contiguous), len = the big-endian u32 header clamped to the available bytes.  grid
 // (ceil(max_len / 4096), inst): thread = 16 output bytes, dword loads/stores when source and
 // destination rows are dword-aligned (byte copy otherwise).
+#if HBX_IN_TU(6)
 __global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards, size_t inst_stride, uint32_t k,
                                               uint32_t L, uint8_t* __restrict__ out, size_t out_stride,
                                               uint64_t* __restrict__ out_len, int32_t* __restrict__ status) {
@@ -872,8 +906,10 @@ __global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards
     for (uint64_t q = 0; q < end; q++) dst[q] = src[q];
   }
 }
+#endif
 
 // status = root(inst) == expected ? status : HBX_E_ROOT_MISMATCH
+#if HBX_IN_TU(6)
 __global__ void k_root_check(const uint8_t* __restrict__ roots, const uint8_t* __restrict__ expect, uint32_t inst,
                              int32_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -882,5 +918,6 @@ __global__ void k_root_check(const uint8_t* __restrict__ roots, const uint8_t* _
   for (int q = 0; q < 32; q++) eq = eq && roots[(size_t)i * 32 + q] == expect[(size_t)i * 32 + q];
   if (!eq) status[i] = -10;
 }
+#endif
 
 }  // namespace hbx

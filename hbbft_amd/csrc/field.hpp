@@ -20,7 +20,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define HBX_HD __host__ __device__ __forceinline__
-#define HBX_HDNI __host__ __device__ __noinline__
+#define HBX_HDNI __host__ __device__ __noinline__ inline
 #else
 #define HBX_HD inline
 #define HBX_HDNI inline

@@ -15,7 +15,11 @@
 #include "../../include/hbx.h"
 #include "hbx_kernels.hip"
 #include "broadcast.hpp"
+#if defined(HBX_TU) && HBX_TU == 0
+#include "_kdecl.hpp"  // the kernels live in translation units 1..6 (tools/build.py)
+#endif
 
+#if !defined(HBX_TU) || HBX_TU == 0
 using namespace hbx;
 
 namespace {
@@ -76,6 +80,8 @@ struct hbx_ctx {
   // verification state: n_shares / verified_p of the last verify after the latest prepare
   // (0 = none: a prepare invalidates S / valid for the combine)
   uint32_t n_shares = 0, verified_p = 0;
+  const uint8_t* early_shares = nullptr;  // shares decoded by the last prepare (prepare_impl)
+  uint32_t early_n = 0;
   dbuf S, S_status, fallback, valid, shares_own, present_own;
   // combine state
   dbuf keys, status, out_own;
@@ -524,9 +530,11 @@ int hbx_set_own_share(hbx_ctx* c, uint32_t me, const uint8_t* sk32) {
   return HBX_OK;
 }
 
-int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
-                              const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
-                              uint64_t max_v_len, uint8_t* d_ct_valid, void* stream) {
+// Ciphertext preparation; with `early_shares` (the fused epoch call) the received shares of the
+// epoch are decoded in the same launch, in waves beside the hash chains.
+static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob, const uint64_t* d_v_off,
+                        const uint8_t* d_w_comp, uint32_t p, uint64_t max_v_len, uint8_t* d_ct_valid,
+                        void* stream, const uint8_t* early_shares, uint32_t early_n) {
   if (!c || p == 0 || !d_u_comp || !d_v_off || !d_w_comp)
     return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
@@ -536,37 +544,46 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
       !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
       !c->ct_valid.ensure(p) || !c->dec_st.ensure((size_t)2 * p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
+  const size_t m_early = early_shares ? (size_t)early_n * p : 0;
+  if (m_early && (!c->S.ensure(m_early * sizeof(g1a)) || !c->S_status.ensure(m_early * 4)))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
   const dim3 b64(64);
+  const bool own = c->own_me != UINT32_MAX;
+  // own entry of the early-decoded matrix (written by k_prepare_lines), as hbx_verify_dec_shares_d
+  const uint32_t me_early = (own && c->own_me < early_n) ? c->own_me : UINT32_MAX;
   {
     timed t_(c, HBX_K_PREPARE_CT, s);
     const uint32_t hash_blocks = (uint32_t)(((size_t)p * HASH_K + 63) / 64);
-    const bool own = c->own_me != UINT32_MAX;
     const uint32_t dec_blocks = (own ? 4 : 2) * ((p + 63) / 64);  // wave-aligned parts (k_prepare_ct)
+    const uint32_t share_blocks = (uint32_t)((m_early + 63) / 64);
     if (own && (!c->own_S.ensure((size_t)p * sizeof(g1a)) || !c->own_part.ensure((size_t)2 * p * sizeof(g1j))))
       return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
-    // HBX_SPLIT_PREP=1 (profiling): the hash part and the decode part as two launches, so a
+    // HBX_SPLIT_PREP=1 (profiling): the hash part and the decode parts as two launches, so a
     // kernel trace times each chain on its own
     static const bool split = getenv("HBX_SPLIT_PREP") != nullptr;
     const uint32_t parts = split ? 2 : 1;
     for (uint32_t q = 0; q < parts; q++) {
       const uint32_t b0 = split && q == 1 ? hash_blocks : 0;
-      const uint32_t nb = split ? (q == 0 ? hash_blocks : dec_blocks) : hash_blocks + dec_blocks;
+      const uint32_t nb = split ? (q == 0 ? hash_blocks : dec_blocks + share_blocks)
+                                : hash_blocks + dec_blocks + share_blocks;
       hipLaunchKernelGGL(k_prepare_ct, dim3(nb), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, hash_blocks,
                          c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
                          own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->digest,
-                         b0);
+                         b0, dec_blocks, early_shares, m_early, early_n ? early_n : 1u, me_early, c->S.as<g1a>(),
+                         c->S_status.as<int32_t>());
     }
     c->own_ready = own;
   }
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    const bool own = c->own_ready;
     const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
+    const bool own_entry = m_early && me_early != UINT32_MAX;
     hipLaunchKernelGGL(k_prepare_lines, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
-                       own ? c->own_S.as<g1a>() : nullptr);
+                       own ? c->own_S.as<g1a>() : nullptr, early_n, me_early,
+                       own_entry ? c->S.as<g1a>() : nullptr, own_entry ? c->S_status.as<int32_t>() : nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = 2 * p * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), b64, 0, s, c->lines.as<line_pre>(),
@@ -577,6 +594,8 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   c->ct_known = false;
   c->n_shares = 0;  // S / valid of an earlier verify belong to other ciphertexts
   c->verified_p = 0;
+  c->early_shares = early_shares;
+  c->early_n = early_n;
   if (d_ct_valid) {
     // Ciphertext::verify now: one check per proposer (n = 0 share jobs, job 0 = the ciphertext)
     if (!c->S.ensure(sizeof(g1a)) || !c->S_status.ensure(4) || !c->valid.ensure(16))
@@ -590,6 +609,12 @@ int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t
   c->d_v_off = d_v_off;
   c->max_v_len = max_v_len;
   return HBX_OK;
+}
+
+int hbx_prepare_ciphertexts_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_blob,
+                              const uint64_t* d_v_off, const uint8_t* d_w_comp, uint32_t p,
+                              uint64_t max_v_len, uint8_t* d_ct_valid, void* stream) {
+  return prepare_impl(c, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, max_v_len, d_ct_valid, stream, nullptr, 0);
 }
 
 int hbx_prepare_ciphertexts(hbx_ctx* c, const uint8_t* u_comp, const uint8_t* v_blob, const uint64_t* v_off,
@@ -635,10 +660,14 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
   // own-share mode: this node's share is the one computed in prepare, and its check IS
   // Ciphertext::verify (k_verify_shares); otherwise the ciphertext checks run separately
   const bool own = c->own_ready && c->own_me < n;
-  hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, d_shares, m,
-                     c->S.as<g1a>(), c->S_status.as<int32_t>(), n, own ? c->own_me : UINT32_MAX,
-                     own ? c->own_S.as<g1a>() : nullptr);
-  HIPCHK(c, hipGetLastError());
+  if (c->early_shares == d_shares && c->early_n == n) {
+    c->early_shares = nullptr;  // decoded by this epoch's prepare (prepare_impl); used once
+  } else {
+    hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, d_shares, m,
+                       c->S.as<g1a>(), c->S_status.as<int32_t>(), n, own ? c->own_me : UINT32_MAX,
+                       own ? c->own_S.as<g1a>() : nullptr);
+    HIPCHK(c, hipGetLastError());
+  }
   // ciphertext checks (if prepare deferred them): latency-bound, p checks -> 16-lane groups
   if (!c->ct_known && !own) {
     int rc = launch_pair_checks(c, s, n, p, n, n, d_present);
@@ -822,7 +851,8 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
-                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr);
+                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
+                       UINT32_MAX, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
@@ -984,7 +1014,7 @@ int hbx_decrypt_epoch_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
   // Stages in stream order.  (Running Ciphertext::verify on the aux stream beside a speculative
   // combine was measured on MI355X and gained nothing: the combine's 4 waves per proposer already
   // occupy every SIMD, and two single-wave-per-SIMD kernels only time-share the VALU.)
-  int rc = hbx_prepare_ciphertexts_d(c, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, max_v_len, nullptr, stream);
+  int rc = prepare_impl(c, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, max_v_len, nullptr, stream, d_shares, n);
   if (rc) return rc;
   rc = hbx_verify_dec_shares_d(c, d_shares, d_present, n, p, d_valid, stream);
   if (rc) return rc;
@@ -1209,3 +1239,4 @@ int hbx_kernel_time(hbx_ctx* c, int kernel, double* total_ms, uint32_t* launches
   if (launches) *launches = (uint32_t)c->tev[kernel].size();
   return HBX_OK;
 }
+#endif  // host translation unit

@@ -18,6 +18,15 @@
 #include "pairing3.hpp"
 #include "wide.hpp"
 
+// Split build (tools/build.py): the kernels compile in groups, one translation unit per group
+// (-DHBX_TU=1..6: epoch, share checks, producer, wide checks, coin, broadcast); TU 0 is the host
+// API, which sees only their declarations (_kdecl.hpp, generated from these sources).
+#if !defined(HBX_TU)
+#define HBX_IN_TU(n) 1
+#else
+#define HBX_IN_TU(n) (HBX_TU == (n))
+#endif
+
 namespace hbx {
 
 struct line_block {  // lines of one proposer: H then W
@@ -56,6 +65,7 @@ __device__ __forceinline__ bool check2_lds(const line_pre* LA, const g1a& PA, bo
   return fq12_is_one(final_exponentiation_lds(f, gslot));
 }
 
+#if HBX_IN_TU(1)
 __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict__ comp, uint32_t n,
                                                       g1a* __restrict__ out, int32_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -65,10 +75,12 @@ __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict_
   out[i] = p;
   status[i] = st;
 }
+#endif
 
 // Lanes per hash_g2 group (hash.hpp hash_g2_group).
 constexpr int HASH_K = 16;
 
+#if HBX_IN_TU(1)
 // H_j = hash_g1_g2(U_j, V_j) for every proposer, plus the decoding of U_j and W_j, in ONE launch:
 //  * blocks [0, hash_blocks): HASH_K-lane groups, one per proposer (hash_g2_group); the hash reads
 //    only the compressed bytes of U_j, so it does not wait for the decode;
@@ -84,8 +96,24 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
                                                    g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
                                                    const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part,
-                                                   int digest, uint32_t block0) {
+                                                   int digest, uint32_t block0, uint32_t dec_blocks,
+                                                   const uint8_t* __restrict__ shares, size_t share_count,
+                                                   uint32_t n, uint32_t me, g1a* __restrict__ S,
+                                                   int32_t* __restrict__ S_status) {
   const uint32_t bid = blockIdx.x + block0;  // block0 > 0: the decode part launched on its own
+  if (bid >= hash_blocks + dec_blocks) {
+    // early share decode (hbx_decrypt_epoch_d): k_decompress_shares' work in waves of this
+    // launch, beside the hash chains (which leave most SIMDs idle) instead of after them.  The
+    // own-share entries are filled by k_prepare_lines.
+    const size_t i = (size_t)(bid - hash_blocks - dec_blocks) * blockDim.x + threadIdx.x;
+    if (i >= share_count || (uint32_t)(i % n) == me) return;
+    g1a q;
+    int32_t st = g1_decompress(shares + i * 48, q);
+    if (st == HBX_PT_OK && !g1_is_torsion_free(q)) st = HBX_PT_NOT_IN_SUBGROUP;
+    S_status[i] = st;
+    S[i] = q;
+    return;
+  }
   if (bid >= hash_blocks) {
     // decode = pairing 0.14's into_affine: on-curve AND subgroup membership (U in G1, W in G2).
     // Each part starts on a wave boundary (pw = p rounded up to 64) so no wave mixes the G1 and
@@ -134,10 +162,12 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   g2j h;
   if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
 }
+#endif
 
 // Lanes per G2 point in k_prepare_lines.
 constexpr int LINE_K = 16;
 
+#if HBX_IN_TU(1)
 // line_dbl_step (pairing.hpp) on the LINE_K lanes of a group that all hold T: its 26 Fq
 // products as three rounds of independent products, one per lane (10, 14 and 8 lanes busy),
 // exchanged by ds_bpermute; Fq2 products by schoolbook.  Same values mod p as line_dbl_step.
@@ -229,7 +259,8 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
                                                       line_pre* __restrict__ lines, fq2* __restrict__ scratch,
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
                                                       uint8_t* __restrict__ ct_ok, const g1j* __restrict__ own_part,
-                                                      g1a* __restrict__ own_S) {
+                                                      g1a* __restrict__ own_S, uint32_t n, uint32_t me,
+                                                      g1a* __restrict__ S, int32_t* __restrict__ S_status) {
   const uint32_t line_blocks = (count * LINE_K + 63) / 64;
   if (blockIdx.x >= line_blocks) {
     // own share S_j,me = k1 U_j + k2 phi(U_j) (k_prepare_ct's two halves) where U_j decoded
@@ -241,6 +272,10 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
     sh.inf = true;
     if (dec_st[j] == HBX_PT_OK) sh = g1_to_affine(g1_add(own_part[2 * j], own_part[2 * j + 1]));
     own_S[j] = sh;
+    if (S) {  // shares decoded early (k_prepare_ct): the own entry as k_decompress_shares writes it
+      S[(size_t)j * n + me] = sh;
+      S_status[(size_t)j * n + me] = sh.inf ? HBX_PT_INFINITY : HBX_PT_OK;
+    }
     return;
   }
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -288,7 +323,9 @@ __global__ void __launch_bounds__(64) k_normalise_lines(line_pre* __restrict__ l
   g2_normalise_line(l, c2[k]);
   lines[k] = l;
 }
+#endif
 
+#if HBX_IN_TU(2)
 // Share verification, one lane per share (lane = sender i, blockIdx.y = proposer j):
 // e(S_ji, H_j) * e(-pk_i, W_j) == 1 over the prepared lines of H_j / W_j (wave-uniform loads)
 // with one shared final exponentiation.  At N=256 one epoch is 65,536 independent checks: one
@@ -359,7 +396,10 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
     if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
   }
 }
+#endif
 
+constexpr int COMBINE_THREADS = 256;
+constexpr int COMBINE_MAX_T = 4096;
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
 // x = index + 1 (canonical, little-endian limbs out).
 __device__ fr lagrange_at_zero(const uint16_t* idx, int t, int k) {
@@ -380,10 +420,9 @@ __device__ fr lagrange_at_zero(const uint16_t* idx, int t, int k) {
   return fr_from_mont(fr_mul(num, fr_inv(den)));
 }
 
+#if HBX_IN_TU(1)
 // Lagrange combine of the first t valid shares of proposer j (one 256-thread block per
 // proposer), then the hash_bytes key = SHA-256(compress(g)).
-constexpr int COMBINE_THREADS = 256;
-constexpr int COMBINE_MAX_T = 4096;
 
 __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __restrict__ valid,
                                                              const g1a* __restrict__ S, uint32_t n,
@@ -460,6 +499,7 @@ __global__ void __launch_bounds__(64) k_keystream_xor(const uint32_t* __restrict
   for (uint64_t q = 16 * b; q < end; q++) out[off + q] = v_blob[off + q] ^ (uint8_t)ks[q - 16 * b];
 }
 
+#endif
 
 // ----------------------------------------------------------------------------------------------
 // Producer side: scalar multiplications that make the
@@ -483,6 +523,7 @@ __device__ __forceinline__ g1a g1_generator() {
   return g;
 }
 
+#if HBX_IN_TU(3)
 // SecretKey::public_key (threshold_crypto): pk = g1 * sk, one lane per key.
 __global__ void __launch_bounds__(64) k_public_keys(const uint8_t* __restrict__ sk32, uint32_t n,
                                                     uint8_t* __restrict__ pk48) {
@@ -532,6 +573,7 @@ __global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, cons
   const g2j h = hash_g1_g2(uc, v + o, len, digest);
   g2_compress(g2_to_affine(g2_mul_bits(h, k, 256)), w96 + (size_t)j * 96);
 }
+#endif
 
 // ----------------------------------------------------------------------------------------------
 // Wide pairing checks: a 16-lane group per check, 8 checks of ONE
@@ -547,6 +589,7 @@ constexpr int SH_SLOTS = prog::NUM_K + 16;
 constexpr int WIDE_LDS_DWORDS = (SH_SLOTS + WG_GROUPS * PRIV_SLOTS) * wide::SLOT;
 constexpr uint8_t JOB_FALLBACK = 1;
 
+#if HBX_IN_TU(4)
 __device__ __forceinline__ void put_fq(uint32_t* lds, uint32_t off, const fq& a) { wide::lds_store_fq(lds, off, a); }
 
 __global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
@@ -646,7 +689,9 @@ __global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
     fallback[(size_t)j * (n + 1) + q] = needs_fallback ? JOB_FALLBACK : 0;
   }
 }
+#endif
 
+#if HBX_IN_TU(1)
 // One lane per share: decompress S_ji (kept for the verification and the Lagrange combine).
 // Decode = pairing 0.14's into_affine (on-curve and G1 membership), as the reference deserialises
 // a DecryptionShare.  In own-share mode the entry of sender `me` is this node's own share from
@@ -668,7 +713,9 @@ __global__ void __launch_bounds__(256) k_decompress_shares(const uint8_t* __rest
   status[i] = st;
   S[i] = p;
 }
+#endif
 
+#if HBX_IN_TU(4)
 // Identity cases (a point at infinity on either side) that the wide kernel flagged: e(O, Q) = 1.
 __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict__ fallback, const g1a* __restrict__ S,
                                                       const g1a* __restrict__ pk, const g1a* __restrict__ U,
@@ -694,7 +741,9 @@ __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict_
   if (q == n) ct_valid[j] = v ? 1 : 0;
   else valid[(size_t)j * n + q] = v ? 1 : 0;
 }
+#endif
 
+#if HBX_IN_TU(1)
 // Shares of a ciphertext that failed Ciphertext::verify become HBX_SHARE_SKIPPED_CT: the
 // reference never verifies them (honey_badger.rs:371-376), so they are neither valid nor a fault.
 __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid, const uint8_t* __restrict__ ct_valid,
@@ -703,10 +752,12 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
   if (k >= (size_t)n * p) return;
   if (ct_valid[k / n] != HBX_CT_VALID && valid[k] <= HBX_SHARE_VALID) valid[k] = HBX_SHARE_SKIPPED_CT;
 }
+#endif
 
 // ----------------------------------------------------------------------------------------------
 // Common Coin (reference src/common_coin.rs)
 // ----------------------------------------------------------------------------------------------
+#if HBX_IN_TU(5)
 // H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one HASH_K-lane
 // group each.
 __global__ void __launch_bounds__(64) k_hash_nonces(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
@@ -818,7 +869,9 @@ __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
 // on two lanes, 4-bit windows, like k_combine) -- concurrent with the G2 sum instead of a pairing
 // after it.  master_ok = 0 where the combine fails.  One block per (instance, part).
 // status: 0 or -3 (NotEnoughShares).
+#endif
 constexpr int SIGCOMB_THREADS = 256;
+#if HBX_IN_TU(5)
 __device__ __forceinline__ g1j g1j_shfl_xor(const g1j& a, int m) {
   return g1j{fq_shfl_xor(a.x, m), fq_shfl_xor(a.y, m), fq_shfl_xor(a.z, m)};
 }
@@ -943,4 +996,5 @@ __global__ void __launch_bounds__(64) k_sign(const uint8_t* __restrict__ sk32, u
   g2_compress(g2_to_affine(g2_mul_bits(g2_from_affine(H[inst]), k, 256)), out96 + ((size_t)inst * n + i) * 96);
 }
 
+#endif
 }  // namespace hbx

@@ -1,0 +1,21 @@
+# One GPU round trip: parity tests, the default bench line (with the CPU baseline), the
+# shard-of-8 rehearsal and a rocprofv3 kernel-trace summary of the bench -- each step under its
+# own limit, stopping at the first failure.  Usage: gpurun -- bash tools/gpu_round.sh <tag>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+tag=${1:-r}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_pytest_gpu.txt 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${tag}_pytest_gpu.txt; exit 1; }
+tail -2 gpurun_out/${tag}_pytest_gpu.txt
+timeout -k 10 400 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 1; }
+cat gpurun_out/${tag}_bench.json
+timeout -k 10 200 python -u bench.py --shard-of 8 --no-cpu-baseline > gpurun_out/${tag}_bench_shard8.json 2> gpurun_out/${tag}_bench_shard8.err || { echo "shard8 failed"; tail -20 gpurun_out/${tag}_bench_shard8.err; exit 1; }
+cat gpurun_out/${tag}_bench_shard8.json
+if [ "${PROF:-1}" = "1" ]; then
+  R="$GRAFT_REPO_ROOT"
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${tag}_prof" -o run -- python3 -u "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/${tag}_prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${tag}_prof.log"; exit 1; }
+  python3 "$R/tools/kstats.py" "$R/gpurun_out/${tag}_prof/run_results.db" > "$R/gpurun_out/${tag}_kernel_stats.txt" && cat "$R/gpurun_out/${tag}_kernel_stats.txt"
+fi
+echo done
