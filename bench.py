@@ -339,7 +339,7 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "u32 (Fq 12x32-bit Montgomery limbs)",
+        "dtype": "i32 (Fq as 14 signed 28-bit digits, R = 2^392, in the share check; 12 x u32 limbs elsewhere)",
         "data": "synthetic (seeded keys, 1 KiB random contributions, GPU-made ciphertexts/shares, 1/64 foreign-ciphertext shares)",
         "config": {"workload": f"HoneyBadger node-epoch N={n}: {n * n} decryption-share verifies + {n} Ciphertext::verify + "
                                f"{n} combines (t={t}) + decrypt, |v|={args.vlen} B"

@@ -1,0 +1,506 @@
+// Signed 28-bit digit form of the BLS12-381 tower, for the share-check kernel (k_verify_shares).
+//
+// Same field, same tower (Fq2 = Fq[u]/(u^2+1), Fq6 = Fq2[v]/(v^3-(u+1)), Fq12 = Fq6[w]/(w^2-v)) as
+// field.hpp -- the values a check computes are the same elements; only their representation in
+// registers differs:
+//  * an Fq element is 14 signed 32-bit digits of weight 2^(28 i), Montgomery with R' = 2^392, so
+//    a product's result digits come out on the same digit grid as its inputs (no re-cutting of
+//    12 x 32-bit limbs into digits and back around every product, field.hpp's fq_mul);
+//  * additions, subtractions and negations are digit-wise and carry-free (14 independent VALU
+//    ops; the 12-limb carry chain of fq_add / fq_sub is 36 ops plus the wait states gfx950
+//    inserts between carry-dependent instructions);
+//  * an Fq2 product is ONE fused column loop computing both Montgomery reductions: per column
+//    a0 b0 - a1 b1 and (a0 + a1)(b0 + b1) - a0 b0 - a1 b1 from three digit convolutions (Karatsuba)
+//    -- 3 x 196 + 2 x 196 = 980 v_mad instead of 3 x 392 = 1176.
+// Bounds (all arithmetic on a column is exact modulo 2^64, so only the TRUE column value must fit
+// a signed 64-bit word -- intermediate wrap-around of the Karatsuba sum is harmless):
+//  * "normalised" (fqd_norm, every product output): digits 0..12 in [0, 2^28), digit 13 signed;
+//    value in (-p, 2p);
+//  * fqd_mul(a, b): max|a_i| max|b_i| <= 2^59;  fq2d_mul / fq2d_sqr: max|a_i| max|b_i| <= 2^58,
+//    i.e. operands that are sums of at most two normalised values.  The tower functions below
+//    take normalised inputs and return normalised outputs; host builds with HBX_DCHECK assert
+//    the operand bounds (tools/hostcheck).
+// Values: a product needs |a b| < p 2^392; operands here stay below 2^386.  Digit sums between
+// normalisations stay below 8 x 2^28 (int32).
+#pragma once
+#include <math.h>
+#include "field.hpp"
+
+#if defined(HBX_DCHECK) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cstdio>
+#include <cstdlib>
+#define HBX_DBOUND(a, lim)                                                                  \
+  do {                                                                                      \
+    for (int i_ = 0; i_ < 14; i_++)                                                         \
+      if ((a).d[i_] > (int64_t)(lim) || (a).d[i_] < -(int64_t)(lim)) {                      \
+        fprintf(stderr, "fqd bound %s:%d digit %d = %d > %lld\n", __FILE__, __LINE__, i_,   \
+                (a).d[i_], (long long)(lim));                                               \
+        abort();                                                                            \
+      }                                                                                     \
+  } while (0)
+#else
+#define HBX_DBOUND(a, lim) ((void)0)
+#endif
+
+namespace hbx {
+
+struct fqd {
+  int32_t d[14];
+};
+struct fq2d {
+  fqd c0, c1;
+};
+struct fq6d {
+  fq2d c0, c1, c2;
+};
+struct fq12d {
+  fq6d c0, c1;
+};
+
+constexpr int32_t DMASK = 0x0FFFFFFF;
+constexpr int64_t DN = 1ll << 28;  // bound of a normalised digit
+
+HBX_HD fqd fqd_const(const int32_t* c) {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = c[i];
+  return r;
+}
+HBX_HD fqd fqd_zero() {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = 0;
+  return r;
+}
+HBX_HD fqd fqd_add(const fqd& a, const fqd& b) {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = a.d[i] + b.d[i];
+  return r;
+}
+HBX_HD fqd fqd_sub(const fqd& a, const fqd& b) {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = a.d[i] - b.d[i];
+  return r;
+}
+HBX_HD fqd fqd_neg(const fqd& a) {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = -a.d[i];
+  return r;
+}
+HBX_HD fqd fqd_dbl(const fqd& a) { return fqd_add(a, a); }
+// carry propagation: digits 0..12 into [0, 2^28), the signed carry into digit 13 (value kept)
+HBX_HD fqd fqd_norm(const fqd& a) {
+  fqd r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int32_t v = a.d[i] + c;
+    r.d[i] = v & DMASK;
+    c = v >> 28;  // arithmetic: floor division
+  }
+  r.d[13] = a.d[13] + c;
+  return r;
+}
+// Value reduction + carry propagation: x - q p with q = floor(d13 / p13) estimated from the top
+// digit (p13 = p >> 364), then digits 0..12 into [0, 2^28).  For |digits| < 2^31 and |q| < 2^14
+// the result lies in (-1.3 p, 2.3 p) ("reduced"): what keeps values bounded across the tower,
+// since the carry-free additions never subtract p.
+HBX_HD fqd fqd_reduce(const fqd& a) {
+  const int32_t q = (int32_t)floorf((float)a.d[13] * (1.0f / (float)FQ_P28[13]));
+  fqd r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    acc += (int64_t)a.d[i] - (int64_t)q * (int64_t)FQ_P28[i];
+    r.d[i] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
+    acc >>= 28;
+  }
+  r.d[13] = (int32_t)(acc + (int64_t)a.d[13] - (int64_t)q * (int64_t)FQ_P28[13]);
+  return r;
+}
+
+// Montgomery product a b / 2^392 (signed digits; see the bounds above).  Column k of the digit
+// convolution accumulates in int64 (v_mad_i64_i32), the reduction digits m_k = -acc p^-1 mod 2^28
+// in unsigned (v_mad_u64_u32); three a*b and two m*p chains per column for ILP, as fq_mul_body.
+HBX_HD fqd fqd_mul(const fqd& a, const fqd& b) {
+  HBX_COUNT_FQMUL();
+  uint32_t m[14];
+  fqd r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int jlo = k < 14 ? 0 : k - 13;
+    const int jhi = k < 14 ? k : 13;
+    int64_t s0 = acc, s1 = 0, s2 = 0;
+    uint64_t t0 = 0, t1 = 0;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++) {
+      const int64_t pr = (int64_t)a.d[j] * (int64_t)b.d[k - j];
+      if (j % 3 == 0) s0 += pr;
+      else if (j % 3 == 1) s1 += pr;
+      else s2 += pr;
+    }
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++)
+      if (j < k - 1) {
+        if (j & 1) t1 = (uint64_t)m[j] * FQ_P28[k - j] + t1;
+        else t0 = (uint64_t)m[j] * FQ_P28[k - j] + t0;
+      }
+    acc = s0 + s1 + s2 + (int64_t)(t0 + t1);
+    if (k >= 1 && k <= 14) acc += (int64_t)((uint64_t)m[k - 1] * FQ_P28[1]);
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * FQ_INV28) & (uint32_t)DMASK;
+      acc += (int64_t)((uint64_t)m[k] * FQ_P28[0]);  // low 28 bits cancel
+      acc >>= 28;
+    } else {
+      r.d[k - 14] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
+      acc >>= 28;
+    }
+  }
+  r.d[13] = (int32_t)acc;
+  return r;
+}
+// a^2: the a_i a_j (i != j) column terms taken once, doubled
+HBX_HD fqd fqd_sqr(const fqd& a) {
+  HBX_COUNT_FQMUL();
+  uint32_t m[14];
+  int32_t a2[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) a2[i] = a.d[i] * 2;
+  fqd r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int jlo = k < 14 ? 0 : k - 13;
+    const int jhi = k < 14 ? k : 13;
+    int64_t s0 = acc, s1 = 0, s2 = 0;
+    uint64_t t0 = 0, t1 = 0;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++) {
+      if (j > k - j) continue;
+      const int64_t pr = j == k - j ? (int64_t)a.d[j] * (int64_t)a.d[j] : (int64_t)a2[j] * (int64_t)a.d[k - j];
+      if (j % 3 == 0) s0 += pr;
+      else if (j % 3 == 1) s1 += pr;
+      else s2 += pr;
+    }
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++)
+      if (j < k - 1) {
+        if (j & 1) t1 = (uint64_t)m[j] * FQ_P28[k - j] + t1;
+        else t0 = (uint64_t)m[j] * FQ_P28[k - j] + t0;
+      }
+    acc = s0 + s1 + s2 + (int64_t)(t0 + t1);
+    if (k >= 1 && k <= 14) acc += (int64_t)((uint64_t)m[k - 1] * FQ_P28[1]);
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * FQ_INV28) & (uint32_t)DMASK;
+      acc += (int64_t)((uint64_t)m[k] * FQ_P28[0]);
+      acc >>= 28;
+    } else {
+      r.d[k - 14] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
+      acc >>= 28;
+    }
+  }
+  r.d[13] = (int32_t)acc;
+  return r;
+}
+
+// Two Montgomery reductions driven by one column loop: (x, y) with x = sum_k X_k 2^(28k),
+// y = sum_k Y_k 2^(28k) given column by column by `col` (X_k, Y_k exact in int64), returns
+// (x / 2^392, y / 2^392) mod p, normalised.
+template <class Col>
+HBX_HD void fqd_redc2(Col col, fqd& rx, fqd& ry) {
+  uint32_t mx[14], my[14];
+  int64_t ax = 0, ay = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int jlo = k < 14 ? 0 : k - 13;
+    const int jhi = k < 14 ? k : 13;
+    int64_t X, Y;
+    col(k, jlo, jhi, X, Y);
+    uint64_t ux = 0, uy = 0;
+#pragma unroll
+    for (int j = jlo; j <= jhi; j++)
+      if (j < k - 1) {
+        ux = (uint64_t)mx[j] * FQ_P28[k - j] + ux;
+        uy = (uint64_t)my[j] * FQ_P28[k - j] + uy;
+      }
+    ax += X + (int64_t)ux;
+    ay += Y + (int64_t)uy;
+    if (k >= 1 && k <= 14) {
+      ax += (int64_t)((uint64_t)mx[k - 1] * FQ_P28[1]);
+      ay += (int64_t)((uint64_t)my[k - 1] * FQ_P28[1]);
+    }
+    if (k < 14) {
+      mx[k] = ((uint32_t)ax * FQ_INV28) & (uint32_t)DMASK;
+      my[k] = ((uint32_t)ay * FQ_INV28) & (uint32_t)DMASK;
+      ax += (int64_t)((uint64_t)mx[k] * FQ_P28[0]);
+      ay += (int64_t)((uint64_t)my[k] * FQ_P28[0]);
+      ax >>= 28;
+      ay >>= 28;
+    } else {
+      rx.d[k - 14] = (int32_t)((uint32_t)ax & (uint32_t)DMASK);
+      ry.d[k - 14] = (int32_t)((uint32_t)ay & (uint32_t)DMASK);
+      ax >>= 28;
+      ay >>= 28;
+    }
+  }
+  rx.d[13] = (int32_t)ax;
+  ry.d[13] = (int32_t)ay;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fq2
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq2d fq2d_add(const fq2d& a, const fq2d& b) { return fq2d{fqd_add(a.c0, b.c0), fqd_add(a.c1, b.c1)}; }
+HBX_HD fq2d fq2d_sub(const fq2d& a, const fq2d& b) { return fq2d{fqd_sub(a.c0, b.c0), fqd_sub(a.c1, b.c1)}; }
+HBX_HD fq2d fq2d_neg(const fq2d& a) { return fq2d{fqd_neg(a.c0), fqd_neg(a.c1)}; }
+HBX_HD fq2d fq2d_dbl(const fq2d& a) { return fq2d{fqd_dbl(a.c0), fqd_dbl(a.c1)}; }
+HBX_HD fq2d fq2d_conj(const fq2d& a) { return fq2d{a.c0, fqd_neg(a.c1)}; }
+HBX_HD fq2d fq2d_norm(const fq2d& a) { return fq2d{fqd_norm(a.c0), fqd_norm(a.c1)}; }
+HBX_HD fq2d fq2d_reduce(const fq2d& a) { return fq2d{fqd_reduce(a.c0), fqd_reduce(a.c1)}; }
+// times xi = 1 + u
+HBX_HD fq2d fq2d_mul_xi(const fq2d& a) { return fq2d{fqd_sub(a.c0, a.c1), fqd_add(a.c0, a.c1)}; }
+
+// (a0 + a1 u)(b0 + b1 u): column k of  a0 b0 - a1 b1  and  (a0 + a1)(b0 + b1) - a0 b0 - a1 b1.
+// Operands: max|digit| products <= 2^58 (sums of two normalised values).  Output normalised.
+HBX_HD fq2d fq2d_mul(const fq2d& a, const fq2d& b) {
+  HBX_DBOUND(a.c0, 2 * DN); HBX_DBOUND(a.c1, 2 * DN); HBX_DBOUND(b.c0, 2 * DN); HBX_DBOUND(b.c1, 2 * DN);
+  HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL();
+  int32_t sa[14], sb[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    sa[i] = a.c0.d[i] + a.c1.d[i];
+    sb[i] = b.c0.d[i] + b.c1.d[i];
+  }
+  fq2d r;
+  fqd_redc2(
+      [&](int k, int jlo, int jhi, int64_t& X, int64_t& Y) {
+        int64_t t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+        for (int j = jlo; j <= jhi; j++) {
+          t0 += (int64_t)a.c0.d[j] * (int64_t)b.c0.d[k - j];
+          t1 += (int64_t)a.c1.d[j] * (int64_t)b.c1.d[k - j];
+          t2 += (int64_t)sa[j] * (int64_t)sb[k - j];
+        }
+        X = t0 - t1;
+        Y = t2 - t0 - t1;
+      },
+      r.c0, r.c1);
+  return r;
+}
+// a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u, both columns in one loop.  Operand bound as fq2d_mul.
+HBX_HD fq2d fq2d_sqr(const fq2d& a) {
+  HBX_DBOUND(a.c0, 2 * DN); HBX_DBOUND(a.c1, 2 * DN);
+  HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL();
+  int32_t s[14], df[14], a2[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    s[i] = a.c0.d[i] + a.c1.d[i];
+    df[i] = a.c0.d[i] - a.c1.d[i];
+    a2[i] = a.c0.d[i] * 2;
+  }
+  fq2d r;
+  fqd_redc2(
+      [&](int k, int jlo, int jhi, int64_t& X, int64_t& Y) {
+        int64_t x = 0, y = 0;
+#pragma unroll
+        for (int j = jlo; j <= jhi; j++) {
+          x += (int64_t)s[j] * (int64_t)df[k - j];
+          y += (int64_t)a2[j] * (int64_t)a.c1.d[k - j];
+        }
+        X = x;
+        Y = y;
+      },
+      r.c0, r.c1);
+  return r;
+}
+// a * s, s in Fq (two products sharing s)
+HBX_HD fq2d fq2d_mul_fq(const fq2d& a, const fqd& s) {
+  HBX_DBOUND(a.c0, 2 * DN); HBX_DBOUND(a.c1, 2 * DN); HBX_DBOUND(s, 2 * DN);
+  HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL();
+  fq2d r;
+  fqd_redc2(
+      [&](int k, int jlo, int jhi, int64_t& X, int64_t& Y) {
+        int64_t x = 0, y = 0;
+#pragma unroll
+        for (int j = jlo; j <= jhi; j++) {
+          x += (int64_t)a.c0.d[j] * (int64_t)s.d[k - j];
+          y += (int64_t)a.c1.d[j] * (int64_t)s.d[k - j];
+        }
+        X = x;
+        Y = y;
+      },
+      r.c0, r.c1);
+  return r;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fq6, Fq12.  Fq12-level functions take reduced (or conjugated reduced) inputs and return reduced
+// outputs; the Fq6 products inside return carry-normalised sums of at most 7 product outputs
+// (fq6d_norm: digits back to [0, 2^28), value not reduced), which the Fq12 level combines and
+// reduces.
+// ----------------------------------------------------------------------------------------------
+HBX_HD fq6d fq6d_add(const fq6d& a, const fq6d& b) { return fq6d{fq2d_add(a.c0, b.c0), fq2d_add(a.c1, b.c1), fq2d_add(a.c2, b.c2)}; }
+HBX_HD fq6d fq6d_sub(const fq6d& a, const fq6d& b) { return fq6d{fq2d_sub(a.c0, b.c0), fq2d_sub(a.c1, b.c1), fq2d_sub(a.c2, b.c2)}; }
+HBX_HD fq6d fq6d_neg(const fq6d& a) { return fq6d{fq2d_neg(a.c0), fq2d_neg(a.c1), fq2d_neg(a.c2)}; }
+HBX_HD fq6d fq6d_norm(const fq6d& a) { return fq6d{fq2d_norm(a.c0), fq2d_norm(a.c1), fq2d_norm(a.c2)}; }
+HBX_HD fq6d fq6d_reduce(const fq6d& a) { return fq6d{fq2d_reduce(a.c0), fq2d_reduce(a.c1), fq2d_reduce(a.c2)}; }
+HBX_HD fq6d fq6d_mul_v(const fq6d& a) { return fq6d{fq2d_mul_xi(a.c2), a.c0, a.c1}; }
+
+// Karatsuba (6 Fq2 products); the operand sums are sums of two normalised values
+HBX_HD fq6d fq6d_mul(const fq6d& a, const fq6d& b) {
+  const fq2d t0 = fq2d_mul(a.c0, b.c0);
+  const fq2d t1 = fq2d_mul(a.c1, b.c1);
+  const fq2d t2 = fq2d_mul(a.c2, b.c2);
+  const fq2d u0 = fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(b.c1, b.c2));
+  const fq2d u1 = fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(b.c0, b.c1));
+  const fq2d u2 = fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(b.c0, b.c2));
+  const fq2d c0 = fq2d_add(t0, fq2d_mul_xi(fq2d_sub(fq2d_sub(u0, t1), t2)));
+  const fq2d c1 = fq2d_add(fq2d_sub(fq2d_sub(u1, t0), t1), fq2d_mul_xi(t2));
+  const fq2d c2 = fq2d_add(fq2d_sub(fq2d_sub(u2, t0), t2), t1);
+  return fq6d_norm(fq6d{c0, c1, c2});
+}
+// a * (b0 + b1 v)   (5 Fq2 products)
+HBX_HD fq6d fq6d_mul_by_01(const fq6d& a, const fq2d& b0, const fq2d& b1) {
+  const fq2d t0 = fq2d_mul(a.c0, b0);
+  const fq2d t1 = fq2d_mul(a.c1, b1);
+  const fq2d c0 = fq2d_add(t0, fq2d_mul_xi(fq2d_mul(a.c2, b1)));
+  const fq2d c1 = fq2d_sub(fq2d_sub(fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(b0, b1)), t0), t1);
+  const fq2d c2 = fq2d_add(fq2d_mul(a.c2, b0), t1);
+  return fq6d_norm(fq6d{c0, c1, c2});
+}
+// a * (s v), s in Fq
+HBX_HD fq6d fq6d_mul_by_1_fq(const fq6d& a, const fqd& s) {
+  return fq6d{fq2d_mul_xi(fq2d_mul_fq(a.c2, s)), fq2d_mul_fq(a.c0, s), fq2d_mul_fq(a.c1, s)};
+}
+
+HBX_HD fq12d fq12d_conj(const fq12d& a) { return fq12d{a.c0, fq6d_neg(a.c1)}; }
+// conj keeps digits within [-2^28, 2^28]: still "normalised" for the product bounds (|digit| <=
+// 2^28); fq6d_norm restores non-negative low digits where a value feeds additions repeatedly.
+
+HBX_HD fq12d fq12d_mul(const fq12d& a, const fq12d& b) {
+  const fq6d t0 = fq6d_mul(a.c0, b.c0);
+  const fq6d t1 = fq6d_mul(a.c1, b.c1);
+  const fq6d s = fq6d_mul(fq6d_norm(fq6d_add(a.c0, a.c1)), fq6d_norm(fq6d_add(b.c0, b.c1)));
+  return fq12d{fq6d_reduce(fq6d_add(t0, fq6d_mul_v(t1))), fq6d_reduce(fq6d_sub(fq6d_sub(s, t0), t1))};
+}
+// complex squaring: c0 = (a0 + a1)(a0 + v a1) - ab - v ab, c1 = 2 ab
+HBX_HD fq12d fq12d_sqr(const fq12d& a) {
+  const fq6d ab = fq6d_mul(a.c0, a.c1);
+  const fq6d t = fq6d_mul(fq6d_norm(fq6d_add(a.c0, a.c1)), fq6d_norm(fq6d_add(a.c0, fq6d_mul_v(a.c1))));
+  const fq6d c0 = fq6d_sub(fq6d_sub(t, ab), fq6d_mul_v(ab));
+  return fq12d{fq6d_reduce(c0), fq6d_reduce(fq6d_add(ab, ab))};
+}
+// f * (c0 + c1 v + c4 v w), c4 in Fq (a prepared line at a G1 point; field.hpp fq12_mul_by_014_t)
+HBX_HD fq12d fq12d_mul_by_014(const fq12d& f, const fq2d& c0, const fq2d& c1, const fqd& c4) {
+  const fq6d aa = fq6d_mul_by_01(f.c0, c0, c1);
+  const fq6d bb = fq6d_mul_by_1_fq(f.c1, c4);
+  const fq2d o = fq2d{fqd_add(c1.c0, c4), c1.c1};
+  const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, fq2d_norm(o));
+  return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bb), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bb))};
+}
+
+// Granger-Scott cyclotomic squaring (field.hpp fq12_cyclotomic_sqr_t)
+HBX_HD void fq4d_sqr(const fq2d& a, const fq2d& b, fq2d& c0, fq2d& c1) {
+  const fq2d t0 = fq2d_sqr(a);
+  const fq2d t1 = fq2d_sqr(b);
+  // carry-normalised (3 product outputs each): the callers take 3 c - 2 z, which must stay
+  // within int32 digits
+  c0 = fq2d_norm(fq2d_add(fq2d_mul_xi(t1), t0));
+  c1 = fq2d_norm(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(a, b)), t0), t1));
+}
+HBX_HD fq12d fq12d_cyclotomic_sqr(const fq12d& f) {
+  fq2d z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
+  fq2d z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fq2d t0, t1, t2, t3;
+  fq4d_sqr(z0, z1, t0, t1);
+  z0 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t0, z0)), t0));
+  z1 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t1, z1)), t1));
+  fq4d_sqr(z2, z3, t0, t1);
+  fq4d_sqr(z4, z5, t2, t3);
+  z4 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t0, z4)), t0));
+  z5 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t1, z5)), t1));
+  t0 = fq2d_mul_xi(t3);
+  z2 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t0, z2)), t0));
+  z3 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t2, z3)), t2));
+  return fq12d{fq6d{z0, z4, z3}, fq6d{z2, z1, z5}};
+}
+
+// Frobenius maps (field.hpp fq12_frobenius / fq12_frobenius2) with the digit-form constants
+HBX_HD fq2d fq2d_const(const int32_t* c0, const int32_t* c1) { return fq2d{fqd_const(c0), fqd_const(c1)}; }
+HBX_HD fq12d fq12d_frobenius(const fq12d& a) {
+  fq12d r;
+  r.c0.c0 = fq2d_norm(fq2d_conj(a.c0.c0));
+  r.c1.c0 = fq2d_mul(fq2d_conj(a.c1.c0), fq2d_const(FROBD1_C1_0, FROBD1_C1_1));
+  r.c0.c1 = fq2d_mul(fq2d_conj(a.c0.c1), fq2d_const(FROBD1_C2_0, FROBD1_C2_1));
+  r.c1.c1 = fq2d_mul(fq2d_conj(a.c1.c1), fq2d_const(FROBD1_C3_0, FROBD1_C3_1));
+  r.c0.c2 = fq2d_mul(fq2d_conj(a.c0.c2), fq2d_const(FROBD1_C4_0, FROBD1_C4_1));
+  r.c1.c2 = fq2d_mul(fq2d_conj(a.c1.c2), fq2d_const(FROBD1_C5_0, FROBD1_C5_1));
+  return r;
+}
+HBX_HD fq12d fq12d_frobenius2(const fq12d& a) {
+  fq12d r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fq2d_mul_fq(a.c1.c0, fqd_const(FROBD2_C1));
+  r.c0.c1 = fq2d_mul_fq(a.c0.c1, fqd_const(FROBD2_C2));
+  r.c1.c1 = fq2d_mul_fq(a.c1.c1, fqd_const(FROBD2_C3));
+  r.c0.c2 = fq2d_mul_fq(a.c0.c2, fqd_const(FROBD2_C4));
+  r.c1.c2 = fq2d_mul_fq(a.c1.c2, fqd_const(FROBD2_C5));
+  return r;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Conversions with field.hpp's 12 x 32-bit form (R = 2^384, lazy [0, 2p])
+// ----------------------------------------------------------------------------------------------
+HBX_HD fqd fqd_from_fq(const fq& a) {
+  fqd raw;  // the 384-bit integer a R in 28-bit digits (non-negative, < 2^384)
+#pragma unroll
+  for (int j = 0; j < 14; j++) {
+    const int bit = 28 * j, w = bit >> 5, sh = bit & 31;
+    uint32_t v = a.l[w] >> sh;
+    if (sh > 4 && w + 1 < 12) v |= a.l[w + 1] << (32 - sh);
+    raw.d[j] = (int32_t)(j == 13 ? v : (v & (uint32_t)DMASK));
+  }
+  return fqd_mul(raw, fqd_const(FQD_CONV));  // (x R) 2^400 / 2^392 = x R 2^8 = x R'
+}
+HBX_HD fq fqd_to_fq(const fqd& a) {
+  // x R' * 2^384 / 2^392 = x R, value in (-p, 2p); + 2p -> (p, 4p), then into [0, 2p)
+  const fqd b = fqd_norm(fqd_add(fqd_mul(a, fqd_const(FQD_BACK)), fqd_const(FQD_2P)));
+  fq r;
+#pragma unroll
+  for (int w = 0; w < 12; w++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int off = 28 * i;
+      if (off + 28 <= 32 * w && i != 13) continue;
+      if (off >= 32 * w + 32) continue;
+      const uint32_t di = (uint32_t)b.d[i];
+      if (off >= 32 * w) v |= di << (off - 32 * w);
+      else v |= di >> (32 * w - off);
+    }
+    r.l[w] = v;
+  }
+  return fq_csub(r, FQ_2P);
+}
+HBX_HD fq2d fq2d_from_fq2(const fq2& a) { return fq2d{fqd_from_fq(a.c0), fqd_from_fq(a.c1)}; }
+HBX_HD fq2 fq2d_to_fq2(const fq2d& a) { return fq2{fqd_to_fq(a.c0), fqd_to_fq(a.c1)}; }
+HBX_HD fq6d fq6d_from_fq6(const fq6& a) { return fq6d{fq2d_from_fq2(a.c0), fq2d_from_fq2(a.c1), fq2d_from_fq2(a.c2)}; }
+HBX_HD fq6 fq6d_to_fq6(const fq6d& a) { return fq6{fq2d_to_fq2(a.c0), fq2d_to_fq2(a.c1), fq2d_to_fq2(a.c2)}; }
+HBX_HD fq12d fq12d_from_fq12(const fq12& a) { return fq12d{fq6d_from_fq6(a.c0), fq6d_from_fq6(a.c1)}; }
+HBX_HD fq12 fq12d_to_fq12(const fq12d& a) { return fq12{fq6d_to_fq6(a.c0), fq6d_to_fq6(a.c1)}; }
+HBX_HD fq12d fq12d_one() {
+  fq12d r;
+  const fqd z = fqd_zero();
+  r.c0 = fq6d{fq2d{fqd_const(FQD_ONE), z}, fq2d{z, z}, fq2d{z, z}};
+  r.c1 = fq6d{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
+  return r;
+}
+// Inversion (once per check) through field.hpp's binary-Euclid inverse
+HBX_HDNI fq12d fq12d_inv(const fq12d& a) { return fq12d_from_fq12(fq12_inv(fq12d_to_fq12(a))); }
+HBX_HDNI bool fq12d_is_one(const fq12d& a) { return fq12_is_one(fq12d_to_fq12(a)); }
+
+}  // namespace hbx

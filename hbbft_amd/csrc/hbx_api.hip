@@ -66,7 +66,7 @@ struct hbx_ctx {
   dbuf pk, pk_status, pk_comp;
   // epoch state
   uint32_t p_ct = 0;
-  dbuf U, G2pts, lines, scratch, ct_ok, ct_valid, dec_st;
+  dbuf U, G2pts, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
   // own-share mode (hbx_set_own_share): this node's index and secret share (8 LE limbs), and its
   // own decryption shares of the prepared ciphertexts
   uint32_t own_me = UINT32_MAX;
@@ -435,7 +435,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part};
+                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -540,7 +540,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) ||
-      !c->lines.ensure((size_t)p * sizeof(line_block)) ||
+      !c->lines.ensure((size_t)p * sizeof(line_block)) || !c->lines_d.ensure((size_t)p * sizeof(line_block_d)) ||
       !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
       !c->ct_valid.ensure(p) || !c->dec_st.ensure((size_t)2 * p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
@@ -587,7 +587,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = 2 * p * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), b64, 0, s, c->lines.as<line_pre>(),
-                       c->scratch.as<fq2>(), nl);
+                       c->scratch.as<fq2>(), nl, c->lines_d.as<line_pre_d>());
   }
   HIPCHK(c, hipGetLastError());
   c->p_ct = p;
@@ -689,7 +689,7 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     else
       hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
                          c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
-                         c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
+                         c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
                          own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
   }
@@ -856,7 +856,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                       c->coin_scratch.as<fq2>(), nl);
+                       c->coin_scratch.as<fq2>(), nl, nullptr);
   }
   HIPCHK(c, hipGetLastError());
   if (h96) {

@@ -16,6 +16,7 @@
 #include "hash.hpp"
 #include "pairing.hpp"
 #include "pairing3.hpp"
+#include "pairingd.hpp"
 #include "wide.hpp"
 
 // Split build (tools/build.py): the kernels compile in groups, one translation unit per group
@@ -32,6 +33,10 @@ namespace hbx {
 struct line_block {  // lines of one proposer: H then W
   line_pre h[MILLER_LINES];
   line_pre w[MILLER_LINES];
+};
+struct line_block_d {  // the same lines in the share check's digit form (pairingd.hpp)
+  line_pre_d h[MILLER_LINES];
+  line_pre_d w[MILLER_LINES];
 };
 
 // Status of a share before its pairing check (include/hbx.h HBX_SHARE_*): HBX_SHARE_VALID means
@@ -316,12 +321,14 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
 // used to sit at the end of each point's sequential chain: the chain of k_prepare_lines is the
 // 68 T steps only, and this launch is 68x wider and one inversion deep.
 __global__ void __launch_bounds__(64) k_normalise_lines(line_pre* __restrict__ lines,
-                                                        const fq2* __restrict__ c2, uint32_t count) {
+                                                        const fq2* __restrict__ c2, uint32_t count,
+                                                        line_pre_d* __restrict__ lines_d) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
   line_pre l = lines[k];
   g2_normalise_line(l, c2[k]);
   lines[k] = l;
+  if (lines_d) lines_d[k] = line_to_d(l);
 }
 #endif
 
@@ -341,11 +348,11 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                                                       const uint8_t* __restrict__ present,
                                                       const g1a* __restrict__ pk, uint32_t n_keys,
                                                       const g2a* __restrict__ G2pts,
-                                                      const line_block* __restrict__ lines,
+                                                      const line_block_d* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
                                                       uint8_t* __restrict__ valid, uint32_t me,
                                                       uint8_t* __restrict__ ct_valid) {
-  __shared__ uint32_t gslots[144 * LDS_FQ12_STRIDE];  // final-exponentiation base, one slot per lane
+  __shared__ uint32_t gslots[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // final-exp base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
@@ -354,10 +361,17 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                                      ct_ok[j] != 0);
   bool v = false;
   if (res == HBX_SHARE_VALID) {
-    g1a npk = pk[i];
-    npk.y = fq_neg(npk.y);
-    v = check2_lds(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf,
-                   (lds_u32*)(gslots + threadIdx.x));
+    // check2_lds in the signed-digit tower (pairingd.hpp): Miller loop and final exponentiation
+    const g1a sh = S[idx], pki = pk[i];
+    const bool skipA = sh.inf || G2pts[2 * j].inf;
+    const bool skipB = pki.inf || G2pts[2 * j + 1].inf;
+    if (skipA && skipB) {
+      v = true;
+    } else {
+      const fq12d fd = miller_loop2_d(lines[j].h, fqd_from_fq(sh.x), fqd_from_fq(sh.y), !skipA, lines[j].w,
+                                      fqd_from_fq(pki.x), fqd_neg(fqd_from_fq(pki.y)), !skipB);
+      v = fq12d_is_one(final_exponentiation_d(fd, (lds_u32*)(gslots + threadIdx.x)));
+    }
   }
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
   if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;

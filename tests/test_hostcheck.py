@@ -18,11 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.fixture(scope="module")
 def hc(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("hostcheck") / "libhostcheck.so")
-    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-o", out,
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-DHBX_DCHECK", "-shared", "-fPIC", "-o", out,
                            os.path.join(ROOT, "tools", "hostcheck", "hostcheck.cpp")])
     lib = ctypes.CDLL(out)
     lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     lib.hc_hash_g1_g2.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    lib.hc_fq2d_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
     return lib
 
 
@@ -121,6 +122,50 @@ def test_pairing_check(hc):
     assert hc.hc_pairing_check2(pa, g2, ng1, qa) == 1          # e(aP,Q) e(-P,aQ) == 1
     qb = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a + 1))
     assert hc.hc_pairing_check2(pa, g2, ng1, qb) == 0
+
+
+def test_digit_tower_products(hc):
+    """fieldd.hpp (the share check's signed 28-bit digit tower, R' = 2^392): Fq and fused Fq2
+    products / squares equal the field's, including the extremes."""
+    rnd = random.Random(21)
+    P = bls.P
+    vals = [0, 1, P - 1, P - 2, (P - 1) // 2] + [rnd.randrange(P) for _ in range(150)]
+    for a in vals:
+        b = rnd.choice(vals)
+        out = ctypes.create_string_buffer(48)
+        hc.hc_fqd_mul(_be(a), _be(b), out)
+        assert int.from_bytes(out.raw, "big") == a * b % P
+    for sq in (0, 1):
+        for _ in range(150):
+            a0, a1, b0, b1 = (rnd.choice(vals) for _ in range(4))
+            if sq:
+                b0, b1 = a0, a1
+            out = ctypes.create_string_buffer(96)
+            hc.hc_fq2d_mul(_be(a0) + _be(a1), _be(b0) + _be(b1), out, sq)
+            assert int.from_bytes(out.raw[:48], "big") == (a0 * b0 - a1 * b1) % P
+            assert int.from_bytes(out.raw[48:], "big") == (a0 * b1 + a1 * b0) % P
+
+
+def test_digit_tower_pairing_check(hc):
+    """The share check's digit-form Miller loop and final exponentiation (pairingd.hpp, the code
+    of k_verify_shares) give the same Fq12 elements as pairing.hpp's on the same prepared lines,
+    for valid and invalid checks; host build with the operand-bound assertions (HBX_DCHECK)."""
+    rnd = random.Random(22)
+    chk = ctypes.c_int()
+    for trial in range(6):
+        a = rnd.randrange(1, bls.R)
+        pa = bls.g1_compress(bls.g1_mul(bls.G1_GEN, a))
+        qa = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+        ng1 = bls.g1_compress(bls.g1_neg(bls.g1_mul(bls.G1_GEN, rnd.randrange(1, bls.R))))
+        qb = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a + (trial & 1)))
+        assert hc.hc_miller2_digit_cmp(pa, qa, ng1, qb, ctypes.byref(chk)) == 3
+    # a check that holds: e(aP, Q) e(-P, aQ) == 1
+    a = rnd.randrange(1, bls.R)
+    pa = bls.g1_compress(bls.g1_mul(bls.G1_GEN, a))
+    g2 = bls.g2_compress(bls.G2_GEN)
+    ng1 = bls.g1_compress(bls.g1_neg(bls.G1_GEN))
+    qa = bls.g2_compress(bls.g2_mul(bls.G2_GEN, a))
+    assert hc.hc_miller2_digit_cmp(pa, g2, ng1, qa, ctypes.byref(chk)) == 3 and chk.value == 1
 
 
 def test_sha256_and_hash_g1_g2(hc):

@@ -3,6 +3,7 @@
 // (libhbx.so never contains or calls this); see tests/test_hostcheck.py.
 #include <cstring>
 #include "../../hbbft_amd/csrc/pairing.hpp"
+#include "../../hbbft_amd/csrc/pairingd.hpp"
 #include "../../hbbft_amd/csrc/hash.hpp"
 using namespace hbx;
 extern "C" {
@@ -84,6 +85,53 @@ int hc_pairing_check2(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, c
   g2_prepare_lines(QA, LA, scratch);
   g2_prepare_lines(QB, LB, scratch);
   return pairing_check2(LA, PA, LB, PB) ? 1 : 0;
+}
+// The share check's digit-form Miller loop (pairingd.hpp) against pairing.hpp's on the same
+// prepared lines: 1 = the same Fq12 element, and *check = the pairing check through it.
+int hc_miller2_digit_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb, int* check) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK) return -1;
+  if (g1_decompress(pb, PB) != HBX_PT_OK) return -2;
+  if (g2_decompress(qa, QA) != HBX_PT_OK) return -3;
+  if (g2_decompress(qb, QB) != HBX_PT_OK) return -4;
+  static line_pre LA[MILLER_LINES], LB[MILLER_LINES];
+  static line_pre_d DA[MILLER_LINES], DB[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  g2_prepare_lines(QB, LB, scratch);
+  for (int i = 0; i < MILLER_LINES; i++) {
+    DA[i] = line_to_d(LA[i]);
+    DB[i] = line_to_d(LB[i]);
+  }
+  const fq12 f = miller_loop2(LA, PA, true, LB, PB, true);
+  const fq12 g = fq12d_to_fq12(miller_loop2_d(DA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), true, DB,
+                                              fqd_from_fq(PB.x), fqd_from_fq(PB.y), true));
+  const fq* a = &f.c0.c0.c0;
+  const fq* b = &g.c0.c0.c0;
+  int same = 1;
+  for (int i = 0; i < 12; i++) same &= fq_eq(a[i], b[i]) ? 1 : 0;
+  *check = fq12_is_one(final_exponentiation(g)) ? 1 : 0;
+  // the digit-form final exponentiation gives the same element as pairing.hpp's
+  static uint32_t slot[LDS_FQ12D_DWORDS];
+  const fq12 e1 = final_exponentiation(g);
+  const fq12 e2 = fq12d_to_fq12(final_exponentiation_d(fq12d_from_fq12(g), slot));
+  const fq* x = &e1.c0.c0.c0;
+  const fq* y = &e2.c0.c0.c0;
+  int same_fe = 1;
+  for (int i = 0; i < 12; i++) same_fe &= fq_eq(x[i], y[i]) ? 1 : 0;
+  return same + 2 * same_fe;
+}
+// digit-form product against the 12-limb one on canonical inputs: out = canonical a b (BE)
+void hc_fqd_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  const fqd x = fqd_from_fq(fq_to_mont(fq_from_be(a))), y = fqd_from_fq(fq_to_mont(fq_from_be(b)));
+  fq_to_be(fq_from_mont(fqd_to_fq(fqd_mul(x, y))), out);
+}
+void hc_fq2d_mul(const uint8_t* a, const uint8_t* b, uint8_t* out, int sqr) {
+  const fq2d x{fqd_from_fq(fq_to_mont(fq_from_be(a))), fqd_from_fq(fq_to_mont(fq_from_be(a + 48)))};
+  const fq2d y{fqd_from_fq(fq_to_mont(fq_from_be(b))), fqd_from_fq(fq_to_mont(fq_from_be(b + 48)))};
+  const fq2d r = sqr ? fq2d_sqr(x) : fq2d_mul(x, y);
+  fq_to_be(fq_from_mont(fqd_to_fq(r.c0)), out);
+  fq_to_be(fq_from_mont(fqd_to_fq(r.c1)), out + 48);
 }
 // e(PA, QA) e(PB, QB) == 1 with QA prepared and QB's lines generated on the fly
 int hc_pairing_check_mixed(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
