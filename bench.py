@@ -52,15 +52,16 @@ MADS_PER_FQMUL = 288
 # tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
-# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_r02d.sh,
-# profiles/r02d_pmc_hbm_bytes.txt, measured on the round-2 kernel): 3.784e6 KB + 7.062e6 KB per
-# launch.  The accesses are the kernel's scratch traffic at the out-of-line Fq12 calls of the
-# final exponentiation (fq12 operands and results pass through the stack), a width the guide
-# leaves uncalibrated, so the raw counter bytes are reported without the x2 streaming-read
-# correction.  Algorithmic bytes per launch are ~10 MB (shares 48 B + pk + 26 KB of lines per
-# proposer + 1 B out): the kernel is VALU-bound and the traffic (~0.38 TB/s) is not its bound.
-TRAFFIC_N256_BYTES = (3.784e6 + 7.062e6) * 1024
-TRAFFIC_SOURCE = "profiles/r02d_pmc_hbm_bytes.txt (PMC FETCH_SIZE+WRITE_SIZE, round-2 kernel)"
+# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_round.sh PMC=1,
+# profiles/r02i_pmc_hbm.txt, the digit-tower kernel of commit "Share check in a signed 28-bit
+# digit tower"): 5.058e6 KB + 8.544e6 KB per launch.  The accesses are the kernel's scratch
+# traffic (95 spilled VGPRs in the Miller loop, Fq12 operands of the out-of-line Fq12 products of
+# the final exponentiation), a width the guide leaves uncalibrated, so the raw counter bytes are
+# reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~12 MB
+# (shares 48 B + pk + 30 KB of digit-form lines per proposer + 1 B out): the kernel is VALU-bound
+# and the traffic (~0.56 TB/s) is not its bound.
+TRAFFIC_N256_BYTES = (5.058e6 + 8.544e6) * 1024
+TRAFFIC_SOURCE = "profiles/r02i_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
 # The benchmarked node is validator 0: its own decryption shares are computed locally
 # (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
 OWN_INDEX = 0

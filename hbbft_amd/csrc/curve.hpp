@@ -45,8 +45,8 @@ HBX_HD g1j g1_from_affine(const g1a& a) {
   return g1j{a.x, a.y, fq_one()};
 }
 
-// dbl-2009-l (a = 0)
-HBX_HDNI g1j g1_dbl(const g1j& p) {
+// dbl-2009-l (a = 0); g1_dbl_i inlined into hot loops, g1_dbl one out-of-line copy
+HBX_HD g1j g1_dbl_i(const g1j& p) {
   const fq A = fq_sqr_inl(p.x);
   const fq B = fq_sqr_inl(p.y);
   const fq C = fq_sqr_inl(B);
@@ -60,9 +60,10 @@ HBX_HDNI g1j g1_dbl(const g1j& p) {
   const fq Z3 = fq_dbl(fq_mul_inl(p.y, p.z));
   return g1j{X3, Y3, Z3};
 }
+HBX_HDNI g1j g1_dbl(const g1j& p) { return g1_dbl_i(p); }
 
 // add-2007-bl, complete for P == Q / P == -Q / identities.
-HBX_HDNI g1j g1_add(const g1j& p, const g1j& q) {
+HBX_HD g1j g1_add_i(const g1j& p, const g1j& q) {
   if (g1j_is_identity(p)) return q;
   if (g1j_is_identity(q)) return p;
   const fq Z1Z1 = fq_sqr_inl(p.z);
@@ -85,6 +86,7 @@ HBX_HDNI g1j g1_add(const g1j& p, const g1j& q) {
   const fq Z3 = fq_mul_inl(fq_sub(fq_sub(fq_sqr_inl(fq_add(p.z, q.z)), Z1Z1), Z2Z2), H);
   return g1j{X3, Y3, Z3};
 }
+HBX_HDNI g1j g1_add(const g1j& p, const g1j& q) { return g1_add_i(p, q); }
 
 HBX_HD g1j g1_neg(const g1j& p) { return g1j{p.x, fq_neg(p.y), p.z}; }
 
@@ -148,7 +150,7 @@ HBX_HDNI g1j g1_mul_u128(const g1a& P, const uint32_t* k4) {
   g1j acc = g1_identity();
 #pragma unroll 1
   for (int i = 127; i >= 0; i--) {
-    acc = g1_dbl(acc);
+    acc = g1_dbl_i(acc);
     if ((k4[i >> 5] >> (i & 31)) & 1) acc = g1_add_mixed_i(acc, q);
   }
   return acc;
@@ -168,8 +170,9 @@ HBX_HDNI g1j g1_mul_u128_w4(const g1a& P, const uint32_t* k4) {
   g1j acc = tab[k4[3] >> 28];
 #pragma unroll 1
   for (int w = 30; w >= 0; w--) {
-    acc = g1_dbl(g1_dbl(g1_dbl(g1_dbl(acc))));
-    acc = g1_add(acc, tab[(k4[w >> 3] >> ((w & 7) * 4)) & 0xFu]);
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) acc = g1_dbl_i(acc);  // one inlined copy each: acc stays in VGPRs
+    acc = g1_add_i(acc, tab[(k4[w >> 3] >> ((w & 7) * 4)) & 0xFu]);
   }
   return acc;
 }

@@ -414,6 +414,7 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
 
 constexpr int COMBINE_THREADS = 256;
 constexpr int COMBINE_MAX_T = 4096;
+constexpr int COMBINE_LDS_T = 512;  // Lagrange x_k cached in LDS up to this threshold
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
 // x = index + 1 (canonical, little-endian limbs out).
 __device__ fr lagrange_at_zero(const uint16_t* idx, int t, int k) {
@@ -444,22 +445,53 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
                                                              uint32_t* __restrict__ keys,
                                                              int32_t* __restrict__ status, int digest) {
   __shared__ uint16_t idx[COMBINE_MAX_T];
-  __shared__ int s_count;
+  __shared__ int wcnt[COMBINE_THREADS / 64];
+  __shared__ fr xm[COMBINE_LDS_T];  // Montgomery x_k = idx_k + 1 (t <= COMBINE_LDS_T)
+  __shared__ fr nall;               // prod_k x_k
   __shared__ g1j red[COMBINE_THREADS];
   const uint32_t j = blockIdx.x;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    int c = 0;
-    for (uint32_t i = 0; i < n && c < (int)t; i++)
-      if (valid[(size_t)j * n + i] == HBX_SHARE_VALID) idx[c++] = (uint16_t)i;
-    s_count = c;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the first t valid senders in index order (BTreeMap order, honey_badger.rs:328-340): a
+  // block-wide ballot compaction, 256 senders per step
+  int count = 0;
+  for (uint32_t i0 = 0; i0 < n && count < (int)t; i0 += COMBINE_THREADS) {
+    const uint32_t i = i0 + (uint32_t)tid;
+    const bool ok = i < n && valid[(size_t)j * n + i] == HBX_SHARE_VALID;
+    const uint64_t b = __ballot(ok);
+    if (lane == 0) wcnt[wv] = __popcll(b);
+    __syncthreads();
+    int before = count, total = 0;
+    for (int q = 0; q < COMBINE_THREADS / 64; q++) {
+      if (q < wv) before += wcnt[q];
+      total += wcnt[q];
+    }
+    const int pos = before + __popcll(b & ((1ull << lane) - 1));
+    if (ok && pos < (int)t) idx[pos] = (uint16_t)i;
+    count += total;
+    __syncthreads();
   }
-  __syncthreads();
-  const int count = s_count;
   const bool ctv = ct_valid[j] == HBX_CT_VALID;
   if (!ctv || count < (int)t) {
     if (tid == 0) status[j] = !ctv ? -7 : -3;
     return;
+  }
+  // Lagrange numerators shared through LDS: lambda_k = N / (x_k prod_{m != k} (x_m - x_k)) with
+  // N = prod_m x_m (one product per block instead of t - 1 per lane)
+  const bool lds_lag = t <= (uint32_t)COMBINE_LDS_T;
+  if (lds_lag) {
+    for (int k = tid; k < (int)t; k += COMBINE_THREADS) {
+      fr x;
+      for (int q = 0; q < 8; q++) x.l[q] = 0;
+      x.l[0] = (uint32_t)idx[k] + 1;
+      xm[k] = fr_to_mont(x);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      fr nn = xm[0];
+      for (int k = 1; k < (int)t; k++) nn = fr_mul(nn, xm[k]);
+      nall = nn;
+    }
+    __syncthreads();
   }
   // two lanes per share (GLV): lane 2k computes k1 S_k, lane 2k+1 computes k2 phi(S_k) with
   // lambda_k = k1 + k2 lambda -- two independent 128-bit scalar multiplications instead of one
@@ -467,7 +499,16 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   g1j acc = g1_identity();
   for (int q = tid; q < 2 * (int)t; q += COMBINE_THREADS) {
     const int k = q >> 1;
-    const fr lam = lagrange_at_zero(idx, (int)t, k);
+    fr lam;
+    if (lds_lag) {
+      const fr xk = xm[k];
+      fr den = xk;
+      for (int m = 0; m < (int)t; m++)
+        if (m != k) den = fr_mul(den, fr_sub(xm[m], xk));
+      lam = fr_from_mont(fr_mul(nall, fr_inv(den)));
+    } else {
+      lam = lagrange_at_zero(idx, (int)t, k);
+    }
     uint32_t k1[4], k2[4];
     g1_glv_split(lam.l, k1, k2);
     g1a sp = S[(size_t)j * n + idx[k]];
