@@ -93,6 +93,8 @@ struct hbx_ctx {
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
       coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
+  // PublicKey::verify batches (hbx_verify_sigs)
+  dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
@@ -435,7 +437,9 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
-                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d};
+                  &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
+                  &c->vs_pk, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
+                  &c->vs_sig, &c->vs_sig_st, &c->vs_status};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -922,6 +926,54 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
   HIPCHK(c, hipStreamSynchronize(s));
   if (valid_bits) pack_bits(v.data(), m, valid_bits);
   c->coin_n = n;
+  return HBX_OK;
+}
+
+int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off,
+                    const uint8_t* sig96, uint32_t count, uint8_t* status) {
+  if (!c || !pk48 || !msg_off || !sig96 || !status || count == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sigs: bad args");
+  for (uint32_t i = 0; i < count; i++)
+    if (msg_off[i + 1] < msg_off[i]) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sigs: msg_off not monotone");
+  const uint64_t total = msg_off[count];
+  if (total && !msg_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sigs: null blob");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (!c->vs_pk.ensure((size_t)count * 48) || !c->vs_blob.ensure(total ? total : 16) ||
+      !c->vs_off.ensure((size_t)(count + 1) * 8) || !c->vs_H.ensure((size_t)count * sizeof(g2a)) ||
+      !c->vs_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
+      !c->vs_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->vs_sig96.ensure((size_t)count * 96) ||
+      !c->vs_sig.ensure((size_t)count * sizeof(g2a)) || !c->vs_sig_st.ensure((size_t)count * 4) ||
+      !c->vs_status.ensure(count))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sigs: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->vs_pk.p, pk48, (size_t)count * 48, hipMemcpyHostToDevice, s));
+  if (total) HIPCHK(c, hipMemcpyAsync(c->vs_blob.p, msg_blob, total, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->vs_off.p, msg_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->vs_sig96.p, sig96, (size_t)count * 96, hipMemcpyHostToDevice, s));
+  // H_i = hash_g2(msg_i) on lane groups, its Miller lines, the signatures' decode
+  hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s,
+                     c->vs_blob.as<uint8_t>(), c->vs_off.as<uint64_t>(), count, c->vs_H.as<g2a>(), c->digest);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_decompress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_sig96.as<uint8_t>(), (size_t)count,
+                     c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
+                     c->vs_lines.as<line_pre>(), c->vs_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
+                     UINT32_MAX, nullptr, nullptr);
+  HIPCHK(c, hipGetLastError());
+  const uint32_t nl = count * MILLER_LINES;
+  hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->vs_lines.as<line_pre>(),
+                     c->vs_scratch.as<fq2>(), nl, nullptr);
+  HIPCHK(c, hipGetLastError());
+  {
+    timed t_(c, HBX_K_VERIFY_SIG, s);
+    hipLaunchKernelGGL(k_verify_sigs, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_pk.as<uint8_t>(),
+                       c->vs_lines.as<line_pre>(), c->vs_H.as<g2a>(), c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(),
+                       count, c->vs_status.as<uint8_t>());
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(status, c->vs_status.p, count, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   return HBX_OK;
 }
 

@@ -874,6 +874,42 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __rest
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
 }
 
+// PublicKey::verify(sig, msg) for independent (key, message, signature) items -- Dynamic
+// HoneyBadger's signed votes (src/dynamic_honey_badger/votes.rs:151-156) and key-generation
+// messages (dynamic_honey_badger.rs:395-410), SURVEY.md §8(f) row 4: e(pk, H_i) e(-g1, sig) == 1
+// with H_i = hash_g2(msg_i) prepared by k_hash_nonces + k_prepare_lines.  One lane per item (the
+// lines differ per lane, so the mixed loop's plain loads).  The key is decoded here as pairing's
+// into_affine does (curve + G1 membership); an identity key or signature reduces the check to
+// "both are the identity" (e(O, H) = 1, and e(pk, H) = 1 only for pk = O since H != O).
+__global__ void __launch_bounds__(64) k_verify_sigs(const uint8_t* __restrict__ pk48, const line_pre* __restrict__ lines,
+                                                    const g2a* __restrict__ H, const g2a* __restrict__ sig,
+                                                    const int32_t* __restrict__ sig_st, uint32_t count,
+                                                    uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  g1a pk;
+  int32_t st = g1_decompress(pk48 + (size_t)i * 48, pk);
+  if (st == HBX_PT_OK && !g1_is_torsion_free(pk)) st = HBX_PT_NOT_IN_SUBGROUP;
+  const bool pk_ok = st == HBX_PT_OK || st == HBX_PT_INFINITY;
+  const bool sig_ok = sig_st[i] == HBX_PT_OK || sig_st[i] == HBX_PT_INFINITY;
+  if (!pk_ok || !sig_ok) {
+    status[i] = HBX_SHARE_UNDECODABLE;
+    return;
+  }
+  const g2a s = sig[i];
+  bool v;
+  if (pk.inf || s.inf) {
+    v = pk.inf && s.inf;
+  } else {
+    g1a ng;
+    ng.x = fq_from_const(G1_GEN_X);
+    ng.y = fq_neg(fq_from_const(G1_GEN_Y));
+    ng.inf = false;
+    v = check_mixed(lines + (size_t)i * MILLER_LINES, pk, H[i].inf, s, ng);
+  }
+  status[i] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+}
+
 // lambda (canonical Fr, 8 LE limbs) in base X = |x| = 0xd201000000010000: lambda = d0 + d1 X +
 // d2 X^2 + d3 X^3 (lambda < r < X^4), by binary long division (the remainder needs 65 bits
 // between steps: its top bit is carried in `top`).

@@ -52,6 +52,7 @@ EXPORTS = (
     "hbx_sign",
     "hbx_verify_sig_shares",
     "hbx_combine_signatures",
+    "hbx_verify_sigs",
     "hbx_rs_encode_d",
     "hbx_rs_reconstruct_d",
     "hbx_merkle_roots_d",
@@ -140,6 +141,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_sign.argtypes = [P, u8p, u32, u8p]
     lib.hbx_verify_sig_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
     lib.hbx_combine_signatures.argtypes = [P, u8p, u32, u8p, i32p, u8p, u8p]
+    lib.hbx_verify_sigs.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
     lib.hbx_rs_encode_d.argtypes = [P, P, u32, u32, u32, u32, P]
     lib.hbx_rs_reconstruct_d.argtypes = [P, P, P, u32, u32, u32, u32, P, P]
     lib.hbx_merkle_roots_d.argtypes = [P, P, u32, u32, u32, P, P]
@@ -406,6 +408,24 @@ class Context:
         self._check(self.lib.hbx_combine_signatures(self.h, _u8(mpk), t, _u8(sig),
                                                     st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _u8(ok), _u8(par)))
         return sig, st, unpack_bits(ok, count), unpack_bits(par, count)
+
+    def verify_sigs(self, pk48: np.ndarray, msgs, sig96: np.ndarray) -> np.ndarray:
+        """PublicKey::verify(sig_i, msg_i) for independent items (DHB votes, key-generation
+        messages): pk48 uint8[count, 48], msgs = list of bytes, sig96 uint8[count, 96] ->
+        HBX_SHARE_* status uint8[count] (VALID / INVALID / UNDECODABLE)."""
+        pk48 = np.ascontiguousarray(pk48, dtype=np.uint8)
+        sig96 = np.ascontiguousarray(sig96, dtype=np.uint8)
+        count = pk48.shape[0]
+        if len(msgs) != count or sig96.shape[0] != count:
+            raise ValueError("verify_sigs: pk48, msgs and sig96 must have the same count")
+        off = np.zeros(count + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(m) for m in msgs])
+        blob = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros(count, dtype=np.uint8)
+        self._check(self.lib.hbx_verify_sigs(self.h, _u8(pk48), _u8(blob),
+                                             off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _u8(sig96), count,
+                                             _u8(out)))
+        return out
 
     # -- broadcast (torch tensors as HBM buffers) ------------------------------------------------
     def rs_encode_d(self, d_shards, k: int, m: int, stream=None):

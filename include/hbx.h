@@ -284,6 +284,20 @@ int hbx_combine_signatures(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t,
                            int32_t* status, uint8_t* master_ok_bits, uint8_t* parity_bits);
 
 /* ---------------------------------------------------------------------------------------------
+ * Dynamic HoneyBadger / key-generation signatures: threshold_crypto
+ * PublicKey::verify(sig, msg) = e(pk, hash_g2(msg)) == e(g1, sig) for `count` independent items,
+ * each with its own key, message and signature -- the signed votes of
+ * src/dynamic_honey_badger/votes.rs:151-156 (msg = bincode(vote)) and the key-generation messages
+ * of src/dynamic_honey_badger/dynamic_honey_badger.rs:395-410 (msg = bincode(kg_msg)).
+ *   pk48[count][48], sig96[count][96] compressed; msg_off[count + 1] byte offsets into msg_blob.
+ *   status[count] = HBX_SHARE_VALID (true), HBX_SHARE_INVALID (false), HBX_SHARE_UNDECODABLE (the
+ *   key or the signature is not a subgroup point: the reference cannot deserialise it).
+ *   hash_g2 uses the context's digest (hbx_set_digest).  Independent of the coin state.
+ * ------------------------------------------------------------------------------------------- */
+int hbx_verify_sigs(hbx_ctx* ctx, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off,
+                    const uint8_t* sig96, uint32_t count, uint8_t* status);
+
+/* ---------------------------------------------------------------------------------------------
  * Broadcast: Reed-Solomon erasure coding and the Merkle tree over shards (SURVEY.md §8 rows
  * C1-C5d), batched over `inst` broadcast instances.  Device pointers, stream-ordered.
  * Shards of one instance are contiguous: d_shards[inst][k + m][L]; leaf i of an instance is the

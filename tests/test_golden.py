@@ -115,3 +115,26 @@ def test_c5_fixture_against_oracle():
         assert len(p["lemma"]) - 1 == int(g["proof_depth"][j])
         for lv, (h, _sib) in enumerate(p["lemma"]):
             assert h == g["proof_nodes"][j, lv].tobytes()
+
+
+def test_sig_fixture_against_oracle():
+    """tests/golden/sigs_n16.npz (PublicKey::verify items, make_sig_golden.py): every decodable
+    item's verdict and hash_g2 point recomputed by the oracle; every undecodable item rejected by
+    the oracle's into_affine restatement."""
+    d = dict(np.load(os.path.join(GOLDEN, "sigs_n16.npz"), allow_pickle=False))
+    off = d["msg_off"]
+    for i in range(int(d["count"])):
+        msg = d["msg_blob"][int(off[i]):int(off[i + 1])].tobytes()
+        if i % 4 == 0:
+            assert bls.g2_compress(tc.hash_g2(msg)) == d["h"][i].tobytes()
+        try:
+            pk = bls.g1_decompress(d["pk"][i].tobytes())
+            sig = bls.g2_decompress(d["sig"][i].tobytes())
+        except ValueError:
+            assert d["expect"][i] == 3
+            continue
+        if pk is None or sig is None:
+            assert d["expect"][i] == (1 if pk is None and sig is None else 0)
+            continue
+        if i in (0, 6, 7, 14):
+            assert tc.verify_sig(pk, sig, msg) == (d["expect"][i] == 1)

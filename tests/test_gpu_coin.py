@@ -97,3 +97,22 @@ def test_hash_g2_sha3_digest_vs_oracle(hbx_ctx):
         hbx_ctx.set_digest(DIGEST_SHA256)
     for j, m in enumerate(msgs):
         assert bytes(h[j]) == bls.g2_compress(tc.hash_g2(m, "sha3_256")), j
+
+
+@pytest.mark.gpu
+def test_verify_sigs_matches_golden(hbx_ctx):
+    """PublicKey::verify batches (DHB votes votes.rs:151-156, key-generation messages
+    dynamic_honey_badger.rs:395-410) against tests/golden/sigs_n16.npz:
+    valid, wrong message, wrong key, off-subgroup / undecodable signature and key, identity cases."""
+    from hbbft_amd.hbx import DIGEST_SHA256
+
+    d = _load("sigs_n16")
+    hbx_ctx.set_digest(DIGEST_SHA256)
+    off = d["msg_off"]
+    msgs = [d["msg_blob"][int(off[i]):int(off[i + 1])].tobytes() for i in range(len(off) - 1)]
+    st = hbx_ctx.verify_sigs(d["pk"], msgs, d["sig"])
+    np.testing.assert_array_equal(st, d["expect"])
+    # a batch of one and the independence from the coin state: the same verdicts item by item
+    for i in (0, 6, 8, 12):
+        np.testing.assert_array_equal(hbx_ctx.verify_sigs(d["pk"][i:i + 1], msgs[i:i + 1], d["sig"][i:i + 1]),
+                                      d["expect"][i:i + 1])
