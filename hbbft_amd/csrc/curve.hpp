@@ -460,6 +460,28 @@ HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
 }
 
 // Jacobian equality (identities included).
+// Jacobian equality in G1 (X1 Z2^2 == X2 Z1^2 and Y1 Z2^3 == Y2 Z1^3, identities apart)
+HBX_HD bool g1j_eq(const g1j& a, const g1j& b) {
+  const bool ia = g1j_is_identity(a), ib = g1j_is_identity(b);
+  if (ia || ib) return ia && ib;
+  const fq za2 = fq_sqr(a.z), zb2 = fq_sqr(b.z);
+  if (!fq_eq(fq_mul(a.x, zb2), fq_mul(b.x, za2))) return false;
+  return fq_eq(fq_mul(a.y, fq_mul(zb2, b.z)), fq_mul(b.y, fq_mul(za2, a.z)));
+}
+// k P for a small scalar (Horner steps of the bivariate commitment evaluation): left-to-right
+// double-and-add on a Jacobian base
+HBX_HDNI g1j g1j_mul_u64(const g1j& p, uint64_t k) {
+  if (k == 0 || g1j_is_identity(p)) return g1_identity();
+  g1j acc = p;
+  const int top = 63 - __builtin_clzll(k);
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    acc = g1_dbl_i(acc);
+    if ((k >> i) & 1) acc = g1_add_i(acc, p);
+  }
+  return acc;
+}
+
 HBX_HD bool g2j_eq(const g2j& a, const g2j& b) {
   const bool ia = g2j_is_identity(a), ib = g2j_is_identity(b);
   if (ia || ib) return ia && ib;

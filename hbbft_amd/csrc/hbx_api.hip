@@ -95,6 +95,8 @@ struct hbx_ctx {
       coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
   // PublicKey::verify batches (hbx_verify_sigs)
   dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
+  // SyncKeyGen commitment checks (hbx_bivar_rows / hbx_bivar_check_acks)
+  dbuf bv_commit48, bv_C, bv_cst, bv_rows, bv_rows48, bv_pst, bv_ackp, bv_acky, bv_vals, bv_out;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
@@ -439,7 +441,8 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
                   &c->vs_pk, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
-                  &c->vs_sig, &c->vs_sig_st, &c->vs_status};
+                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
+                  &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -973,6 +976,65 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(status, c->vs_status.p, count, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return HBX_OK;
+}
+
+// Decode p commitments of degree t and compute their rows at x (device state for the checks).
+static int bivar_rows_impl(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x, bool want48) {
+  if (!c || !commit48 || p == 0 || t > 4095) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t M = (size_t)(t + 1) * (t + 2) / 2, nr = (size_t)p * (t + 1);
+  if (!c->bv_commit48.ensure(p * M * 48) || !c->bv_C.ensure(p * M * sizeof(g1a)) || !c->bv_cst.ensure(p * M * 4) ||
+      !c->bv_rows.ensure(nr * sizeof(g1j)) || !c->bv_rows48.ensure(nr * 48) || !c->bv_pst.ensure(p))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_bivar: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->bv_commit48.p, commit48, p * M * 48, hipMemcpyHostToDevice, s));
+  // decode = into_affine (curve + G1 membership), as a Part's commitment deserialises
+  hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((p * M + 255) / 256)), dim3(256), 0, s,
+                     c->bv_commit48.as<uint8_t>(), p * M, c->bv_C.as<g1a>(), c->bv_cst.as<int32_t>(), 1u, UINT32_MAX,
+                     nullptr);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_bivar_rows, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, s, c->bv_C.as<g1a>(),
+                     c->bv_cst.as<int32_t>(), p, t, x, c->bv_rows.as<g1j>(), want48 ? c->bv_rows48.as<uint8_t>() : nullptr,
+                     c->bv_pst.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+int hbx_bivar_rows(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x, uint8_t* rows48,
+                   uint8_t* status) {
+  if (!rows48 || !status) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar_rows: null output");
+  int rc = bivar_rows_impl(c, commit48, p, t, x, true);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(rows48, c->bv_rows48.p, (size_t)p * (t + 1) * 48, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(status, c->bv_pst.p, p, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return HBX_OK;
+}
+
+int hbx_bivar_check_acks(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x,
+                         const uint32_t* ack_proposer, const uint64_t* ack_y, const uint8_t* vals32, uint32_t count,
+                         uint8_t* status) {
+  if (!ack_proposer || !ack_y || !vals32 || !status || count == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_bivar_check_acks: bad args");
+  for (uint32_t k = 0; k < count; k++)
+    if (ack_proposer[k] >= p) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar_check_acks: proposer %u >= p", ack_proposer[k]);
+  int rc = bivar_rows_impl(c, commit48, p, t, x, false);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  if (!c->bv_ackp.ensure((size_t)count * 4) || !c->bv_acky.ensure((size_t)count * 8) ||
+      !c->bv_vals.ensure((size_t)count * 32) || !c->bv_out.ensure(count))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_bivar_check_acks: out of device memory");
+  HIPCHK(c, hipMemcpyAsync(c->bv_ackp.p, ack_proposer, (size_t)count * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->bv_acky.p, ack_y, (size_t)count * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(c->bv_vals.p, vals32, (size_t)count * 32, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_bivar_check, dim3((count + 63) / 64), dim3(64), 0, s, c->bv_rows.as<g1j>(),
+                     c->bv_pst.as<uint8_t>(), t, c->bv_ackp.as<uint32_t>(), c->bv_acky.as<uint64_t>(),
+                     c->bv_vals.as<uint8_t>(), count, c->bv_out.as<uint8_t>());
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(status, c->bv_out.p, count, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return HBX_OK;
 }

@@ -628,6 +628,64 @@ __global__ void __launch_bounds__(64) k_encrypt(const g1a* __restrict__ pk, cons
   const g2j h = hash_g1_g2(uc, v + o, len, digest);
   g2_compress(g2_to_affine(g2_mul_bits(h, k, 256)), w96 + (size_t)j * 96);
 }
+
+// ----------------------------------------------------------------------------------------------
+// SyncKeyGen commitment checks (reference src/sync_key_gen.rs): a Part's
+// BivarCommitment C (symmetric, degree t, (t+1)(t+2)/2 G1 points in threshold_crypto's
+// coeff_pos order, j (j + 1)/2 + i for i <= j) and the Ack values sent to this node.
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bivar_pos(uint32_t i, uint32_t j) {
+  return i <= j ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j;
+}
+// BivarCommitment::row(x) (sync_key_gen.rs:313, :401): R_j = sum_i C_ij x^i by Horner in x, one
+// lane per (proposer, j).  pst[q] = HBX_SHARE_UNDECODABLE if any of q's points failed to decode.
+__global__ void __launch_bounds__(64) k_bivar_rows(const g1a* __restrict__ C, const int32_t* __restrict__ cst,
+                                                   uint32_t p, uint32_t t, uint64_t x, g1j* __restrict__ rows,
+                                                   uint8_t* __restrict__ rows48, uint8_t* __restrict__ pst) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p * (t + 1)) return;
+  const uint32_t q = k / (t + 1), j = k % (t + 1);
+  const uint32_t M = (t + 1) * (t + 2) / 2;
+  const g1a* Cq = C + (size_t)q * M;
+  bool ok = true;  // the whole commitment decodes (every lane of q decides the same)
+  for (uint32_t m = 0; m < M; m++) {
+    const int32_t st = cst[(size_t)q * M + m];
+    ok = ok && (st == HBX_PT_OK || st == HBX_PT_INFINITY);
+  }
+  g1j acc = g1_identity();
+  if (ok) {
+    for (int i = (int)t; i >= 0; i--) acc = g1_add_mixed_i(g1j_mul_u64(acc, x), Cq[bivar_pos((uint32_t)i, j)]);
+  }
+  rows[k] = acc;
+  if (rows48) g1_compress(g1_to_affine(acc), rows48 + (size_t)k * 48);
+  if (j == 0) pst[q] = ok ? HBX_SHARE_VALID : HBX_SHARE_UNDECODABLE;
+}
+// handle_ack's value check (sync_key_gen.rs:449): commit.evaluate(x, y) = sum_j R_j y^j (Horner in
+// y) == g1 * val, one lane per ack.  val must be a canonical Fr (big-endian); otherwise, or when
+// the proposer's commitment did not decode, HBX_SHARE_UNDECODABLE.
+__global__ void __launch_bounds__(64) k_bivar_check(const g1j* __restrict__ rows, const uint8_t* __restrict__ pst,
+                                                    uint32_t t, const uint32_t* __restrict__ ack_p,
+                                                    const uint64_t* __restrict__ ack_y,
+                                                    const uint8_t* __restrict__ vals32, uint32_t count,
+                                                    uint8_t* __restrict__ out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint32_t q = ack_p[k];
+  uint32_t v[8];
+  fr_from_be32(vals32 + (size_t)k * 32, v);
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) (void)subb32(v[i], FR_R[i], br);
+  if (pst[q] != HBX_SHARE_VALID || !br) {
+    out[k] = HBX_SHARE_UNDECODABLE;
+    return;
+  }
+  const g1j* R = rows + (size_t)q * (t + 1);
+  g1j acc = g1_identity();
+  for (int j = (int)t; j >= 0; j--) acc = g1_add(g1j_mul_u64(acc, ack_y[k]), R[j]);
+  const g1j rhs = g1_mul_scalar(g1_from_affine(g1_generator()), v);
+  out[k] = g1j_eq(acc, rhs) ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+}
 #endif
 
 // ----------------------------------------------------------------------------------------------

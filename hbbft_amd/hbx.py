@@ -53,6 +53,8 @@ EXPORTS = (
     "hbx_verify_sig_shares",
     "hbx_combine_signatures",
     "hbx_verify_sigs",
+    "hbx_bivar_rows",
+    "hbx_bivar_check_acks",
     "hbx_rs_encode_d",
     "hbx_rs_reconstruct_d",
     "hbx_merkle_roots_d",
@@ -142,6 +144,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_verify_sig_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
     lib.hbx_combine_signatures.argtypes = [P, u8p, u32, u8p, i32p, u8p, u8p]
     lib.hbx_verify_sigs.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
+    lib.hbx_bivar_rows.argtypes = [P, u8p, u32, u32, ctypes.c_uint64, u8p, u8p]
+    lib.hbx_bivar_check_acks.argtypes = [P, u8p, u32, u32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), u64p,
+                                         u8p, u32, u8p]
     lib.hbx_rs_encode_d.argtypes = [P, P, u32, u32, u32, u32, P]
     lib.hbx_rs_reconstruct_d.argtypes = [P, P, P, u32, u32, u32, u32, P, P]
     lib.hbx_merkle_roots_d.argtypes = [P, P, u32, u32, u32, P, P]
@@ -425,6 +430,29 @@ class Context:
         self._check(self.lib.hbx_verify_sigs(self.h, _u8(pk48), _u8(blob),
                                              off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _u8(sig96), count,
                                              _u8(out)))
+        return out
+
+    def bivar_rows(self, commits: np.ndarray, t: int, x: int):
+        """BivarCommitment::row(x) of p commitments uint8[p, (t+1)(t+2)/2, 48] ->
+        (rows uint8[p, t + 1, 48], status uint8[p])."""
+        commits = np.ascontiguousarray(commits, dtype=np.uint8)
+        p = commits.shape[0]
+        rows = np.zeros((p, t + 1, 48), dtype=np.uint8)
+        st = np.zeros(p, dtype=np.uint8)
+        self._check(self.lib.hbx_bivar_rows(self.h, _u8(commits), p, t, x, _u8(rows), _u8(st)))
+        return rows, st
+
+    def bivar_check_acks(self, commits: np.ndarray, t: int, x: int, proposer, y, vals32: np.ndarray) -> np.ndarray:
+        """handle_ack's check commit[proposer].evaluate(x, y) == g1 * val -> HBX_SHARE_* uint8[count]."""
+        commits = np.ascontiguousarray(commits, dtype=np.uint8)
+        pr = np.ascontiguousarray(proposer, dtype=np.uint32)
+        yy = np.ascontiguousarray(y, dtype=np.uint64)
+        vals32 = np.ascontiguousarray(vals32, dtype=np.uint8)
+        out = np.zeros(len(pr), dtype=np.uint8)
+        self._check(self.lib.hbx_bivar_check_acks(self.h, _u8(commits), commits.shape[0], t, x,
+                                                  pr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                  yy.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _u8(vals32),
+                                                  len(pr), _u8(out)))
         return out
 
     # -- broadcast (torch tensors as HBM buffers) ------------------------------------------------

@@ -296,6 +296,22 @@ int hbx_combine_signatures(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t,
  * ------------------------------------------------------------------------------------------- */
 int hbx_verify_sigs(hbx_ctx* ctx, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off,
                     const uint8_t* sig96, uint32_t count, uint8_t* status);
+/* SyncKeyGen (src/sync_key_gen.rs) commitment checks over p Parts' BivarCommitments of degree t:
+ *   commit48[p][(t+1)(t+2)/2][48], compressed, in threshold_crypto's coefficient order
+ *   coeff_pos(i, j) = j (j + 1)/2 + i for i <= j (the symmetric matrix stored once).
+ * hbx_bivar_rows -- BivarCommitment::row(x) (sync_key_gen.rs:313 `commit.row(idx + 1)`, :401):
+ *   rows48[p][t + 1][48] = sum_i C_ij x^i; status[p] = HBX_SHARE_VALID, or HBX_SHARE_UNDECODABLE
+ *   when a point of the commitment is not in G1 (the Part does not deserialise).
+ * hbx_bivar_check_acks -- handle_ack's value check (sync_key_gen.rs:449):
+ *   commit[ack_proposer[k]].evaluate(x, ack_y[k]) == g1 * val_k with val_k = vals32[k] (32-byte
+ *   big-endian Fr; x = our_idx + 1, y = sender_idx + 1).  status[k] = HBX_SHARE_VALID (equal),
+ *   HBX_SHARE_INVALID ("wrong value"), HBX_SHARE_UNDECODABLE (val >= r or the commitment does
+ *   not decode). */
+int hbx_bivar_rows(hbx_ctx* ctx, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x, uint8_t* rows48,
+                   uint8_t* status);
+int hbx_bivar_check_acks(hbx_ctx* ctx, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x,
+                         const uint32_t* ack_proposer, const uint64_t* ack_y, const uint8_t* vals32, uint32_t count,
+                         uint8_t* status);
 
 /* ---------------------------------------------------------------------------------------------
  * Broadcast: Reed-Solomon erasure coding and the Merkle tree over shards (SURVEY.md §8 rows

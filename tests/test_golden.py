@@ -138,3 +138,27 @@ def test_sig_fixture_against_oracle():
             continue
         if i in (0, 6, 7, 14):
             assert tc.verify_sig(pk, sig, msg) == (d["expect"][i] == 1)
+
+
+@pytest.mark.parametrize("name", ["bivar_t2", "bivar_t5"])
+def test_bivar_fixture_against_oracle(name):
+    """tests/golden/bivar_t*.npz (make_bivar_golden.py): rows re-derived from the committed
+    commitment points, and a sample of acks re-evaluated (oracle/bivar.py)."""
+    from oracle import bivar
+
+    d = dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+    t, x = int(d["t"]), int(d["x"])
+    for q in range(int(d["p"])):
+        if d["commit_status"][q] != 1:
+            with pytest.raises(ValueError):
+                [bls.g1_decompress(c.tobytes()) for c in d["commits"][q]]
+            continue
+        commit = [bls.g1_decompress(c.tobytes()) for c in d["commits"][q]]
+        assert [bls.g1_compress(r) for r in bivar.row(commit, t, x)] == [r.tobytes() for r in d["rows"][q]]
+        for k in np.nonzero(d["ack_proposer"] == q)[0][::4]:
+            val = int.from_bytes(d["vals"][k].tobytes(), "big")
+            if val >= bls.R:
+                assert d["expect"][k] == 3
+                continue
+            ok = bivar.evaluate(commit, t, x, int(d["ack_y"][k])) == bls.g1_mul(bls.G1_GEN, val)
+            assert ok == (d["expect"][k] == 1)

@@ -116,3 +116,20 @@ def test_verify_sigs_matches_golden(hbx_ctx):
     for i in (0, 6, 8, 12):
         np.testing.assert_array_equal(hbx_ctx.verify_sigs(d["pk"][i:i + 1], msgs[i:i + 1], d["sig"][i:i + 1]),
                                       d["expect"][i:i + 1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["bivar_t2", "bivar_t5"])
+def test_bivar_commitment_checks_match_golden(hbx_ctx, name):
+    """SyncKeyGen (SURVEY.md §8(f) row 4): BivarCommitment::row(our_idx + 1) (sync_key_gen.rs:313)
+    and handle_ack's value check commit.evaluate(x, y) == g1 * val (:449) against
+    tests/golden/bivar_t{2,5}.npz: row points byte-exact, per-ack status incl. wrong values,
+    non-canonical values and an undecodable commitment."""
+    d = _load(name)
+    t, x = int(d["t"]), int(d["x"])
+    rows, st = hbx_ctx.bivar_rows(d["commits"], t, x)
+    np.testing.assert_array_equal(st, d["commit_status"])
+    ok = d["commit_status"] == 1
+    np.testing.assert_array_equal(rows[ok], d["rows"][ok])
+    out = hbx_ctx.bivar_check_acks(d["commits"], t, x, d["ack_proposer"], d["ack_y"], d["vals"])
+    np.testing.assert_array_equal(out, d["expect"])
