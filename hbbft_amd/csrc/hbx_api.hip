@@ -690,7 +690,7 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     if (three)
       hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
                          c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
-                         c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
+                         c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n,
                          c->valid.as<uint8_t>(), own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
     else

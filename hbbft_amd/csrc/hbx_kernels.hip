@@ -17,6 +17,7 @@
 #include "pairing.hpp"
 #include "pairing3.hpp"
 #include "pairingd.hpp"
+#include "pairing3d.hpp"
 #include "wide.hpp"
 
 // Split build (tools/build.py): the kernels compile in groups, one translation unit per group
@@ -387,7 +388,7 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
                                                        const uint8_t* __restrict__ present,
                                                        const g1a* __restrict__ pk, uint32_t n_keys,
                                                        const g2a* __restrict__ G2pts,
-                                                       const line_block* __restrict__ lines,
+                                                       const line_block_d* __restrict__ lines,
                                                        const uint8_t* __restrict__ ct_ok, uint32_t n,
                                                        uint8_t* __restrict__ valid, uint32_t me,
                                                        uint8_t* __restrict__ ct_valid) {
@@ -403,7 +404,7 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
   if (res == HBX_SHARE_VALID) {
     g1a npk = pk[i];
     npk.y = fq_neg(npk.y);
-    v = check2_g3(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf, g);
+    v = check2_g3d(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf, g);
   }
   if (g.gl == 0) {
     valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
