@@ -442,7 +442,8 @@ HBX_HD g2j g2_psi(const g2j& p) {
 // 507-bit double-and-add, here in ~4x fewer operations:
 //   Q = h_eff P by the psi formula of Budroni-Pintore / IETF hash-to-curve, h_eff = 3(x^2-1) h2;
 //   h2 P = s Q with s = (3(x^2-1))^-1 mod r = D (1 + x - x^2 - x^3), psi = [x] on G2 (Q in G2).
-HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
+// Q = h_eff P (the first half of g2_clear_cofactor)
+HBX_HDNI g2j g2_heff(const g2j& P) {
   const g2j t1 = g2_neg(g2_mul_u64(P, BLS_X));  // [x] P, x = -|x|
   g2j t2 = g2_psi(P);
   g2j t3 = g2_psi(g2_psi(g2_dbl(P)));
@@ -451,7 +452,18 @@ HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
   t2 = g2_neg(g2_mul_u64(t2, BLS_X));
   t3 = g2_add(t3, t2);
   t3 = g2_sub(t3, t1);
-  const g2j Q = g2_sub(t3, P);
+  return g2_sub(t3, P);
+}
+// h2 P from Q = h_eff P (the second half): s Q, s = (3(x^2-1))^-1 mod r
+HBX_HDNI g2j g2_heff_to_h2(const g2j& Q) {
+  const g2j q1 = g2_psi(Q);
+  const g2j q2 = g2_psi(q1);
+  const g2j q3 = g2_psi(q2);
+  const g2j Rp = g2_sub(g2_sub(g2_add(Q, q1), q2), q3);
+  return g2_mul_gls_d(Rp);
+}
+HBX_HDNI g2j g2_clear_cofactor(const g2j& P) {
+  const g2j Q = g2_heff(P);
   const g2j q1 = g2_psi(Q);
   const g2j q2 = g2_psi(q1);
   const g2j q3 = g2_psi(q2);

@@ -489,7 +489,9 @@ __device__ g2j g2_mul_gls_d_group(const g2j& P, int gl, int gbase) {
   acc = GADD(g2_dbl_n_group(acc, 16, gl, gbase), Z);
   return GADD(g2_dbl_n_group(acc, 16, gl, gbase), W);
 }
-__device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
+// full = false stops at Q = h_eff P = [3(x^2-1)] h2 P (k_prepare_ct: the checks carry the factor
+// on their G1 side, hbx_api.hip pk_m / G1_MGEN)
+__device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase, bool full = true) {
   const g2j t1 = g2_neg(g2_mul_u64_group(P, BLS_X, gl, gbase));
   g2j t2 = g2_psi(P);
   g2j t3 = g2_psi(g2_psi(g2_dbl_group(P, gl, gbase)));
@@ -499,6 +501,7 @@ __device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
   t3 = GADD(t3, t2);
   t3 = GSUB(t3, t1);
   const g2j Q = GSUB(t3, P);
+  if (!full) return Q;
   const g2j q1 = g2_psi(Q);
   const g2j q2 = g2_psi(q1);
   const g2j q3 = g2_psi(q2);
@@ -523,7 +526,7 @@ __device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase) {
 #define HBX_PHASE(k)  // profiling hook (tools/microbench/hashg2.hip records wall-clock stamps)
 #endif
 template <int K>
-__device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
+__device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out, bool full = true) {
   static_assert(K >= 8 && K <= 32 && (64 % K) == 0, "group size (the cofactor clearing uses 8 lanes)");
   if (!active) return false;
   const int lane = (int)(threadIdx.x & 63);
@@ -570,7 +573,7 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out) {
     const int src = gbase + win;
     const fq2 xw = fq2{fq_from_lane(x.c0, src), fq_from_lane(x.c1, src)};
     const fq2 yw = fq2{fq_from_lane(y.c0, src), fq_from_lane(y.c1, src)};
-    out = g2_clear_cofactor_group(g2j{xw, yw, fq2_one()}, gl, gbase);
+    out = g2_clear_cofactor_group(g2j{xw, yw, fq2_one()}, gl, gbase, full);
     HBX_PHASE(4);
     const bool ident = g2j_is_identity(out);
     if ((__ballot(ident) & gmask) == 0) return gl == win;

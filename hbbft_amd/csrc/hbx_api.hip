@@ -63,7 +63,7 @@ struct hbx_ctx {
   int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1 or 3 lanes per share check
   // era state
   uint32_t n_keys = 0;
-  dbuf pk, pk_status, pk_comp;
+  dbuf pk, pk_m, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk (k_scale_keys)
   // epoch state
   uint32_t p_ct = 0;
   dbuf U, G2pts, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
@@ -179,14 +179,14 @@ static int launch_pair_checks(hbx_ctx* c, hipStream_t s, uint32_t n, uint32_t p,
   {
     timed t_(c, HBX_K_CT_CHECKS, s);
     hipLaunchKernelGGL(k_verify_wide, dim3((jobs + WG_GROUPS - 1) / WG_GROUPS, p), dim3(WG_THREADS), 0, s,
-                       c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
+                       c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,
                        c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(), c->ct_ok.as<uint8_t>(), n,
                        q_first, q_last, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>(), c->fallback.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());
   const size_t all = (size_t)p * (n + 1);
   hipLaunchKernelGGL(k_pair_fallback, dim3((unsigned)((all + 63) / 64)), dim3(64), 0, s, c->fallback.as<uint8_t>(),
-                     c->S.as<g1a>(), c->pk.as<g1a>(), c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(),
+                     c->S.as<g1a>(), c->pk_m.as<g1a>(), c->U.as<g1a>(), c->G2pts.as<g2a>(), c->lines.as<line_block>(),
                      n, p, c->valid.as<uint8_t>(), c->ct_valid.as<uint8_t>());
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
@@ -429,7 +429,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
-  dbuf* bufs[] = {&c->pk,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
+  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback,
@@ -490,13 +490,17 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
   c->n_shares = 0;
   c->verified_p = 0;
   c->coin_n = 0;
-  if (!c->pk.ensure((size_t)n * sizeof(g1a)) || !c->pk_status.ensure((size_t)n * 4) ||
-      !c->pk_comp.ensure((size_t)n * 48))
+  if (!c->pk.ensure((size_t)n * sizeof(g1a)) || !c->pk_m.ensure((size_t)n * sizeof(g1a)) ||
+      !c->pk_status.ensure((size_t)n * 4) || !c->pk_comp.ensure((size_t)n * 48))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_pk_shares: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->pk_comp.p, pk_comp, (size_t)n * 48, hipMemcpyHostToDevice, c->stream));
   if (n) {
     hipLaunchKernelGGL(k_decompress_g1, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->pk_comp.as<uint8_t>(),
                        n, c->pk.as<g1a>(), c->pk_status.as<int32_t>());
+    HIPCHK(c, hipGetLastError());
+    // [3(x^2-1)] pk_i: the decryption-share checks' G1 side against H' = h_eff P (k_prepare_ct)
+    hipLaunchKernelGGL(k_scale_keys, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->pk.as<g1a>(), n,
+                       c->pk_m.as<g1a>());
     HIPCHK(c, hipGetLastError());
   }
   std::vector<int32_t> st(n);
@@ -689,13 +693,13 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     const bool three = c->verify_lanes == 3 || (c->verify_lanes == 0 && waves1 < (size_t)VERIFY_FILL_WAVES);
     if (three)
       hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
-                         c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys,
+                         c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,
                          c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n,
                          c->valid.as<uint8_t>(), own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
     else
       hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
-                         c->S_status.as<int32_t>(), d_present, c->pk.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
+                         c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
                          c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
                          own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
@@ -1188,8 +1192,9 @@ int hbx_get_ct_hashes(hbx_ctx* c, uint8_t* h96, size_t count) {
   HIPCHK(c, hipDeviceSynchronize());
   dbuf out;
   if (!out.ensure(count * 96)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_get_ct_hashes: out of device memory");
-  hipLaunchKernelGGL(k_compress_g2, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, c->stream, c->G2pts.as<g2a>(),
-                     (uint32_t)count, 2u, out.as<uint8_t>());
+  // G2pts holds H' = h_eff P = [3(x^2-1)] H (k_prepare_ct); the reference's H = h2 P from it
+  hipLaunchKernelGGL(k_true_hashes, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, c->stream, c->G2pts.as<g2a>(),
+                     (uint32_t)count, out.as<uint8_t>());
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) e = hipMemcpy(h96, out.p, count * 96, hipMemcpyDeviceToHost);

@@ -166,7 +166,10 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   uint8_t d[32];
   hash_g1_g2_digest(u_comp + (size_t)j * 48, v_blob + off, len, d, digest);
   g2j h;
-  if (hash_g2_group<HASH_K>(d, true, h)) G2pts[2 * j] = g2_to_affine(h);
+  // H'_j = h_eff P = [3(x^2-1)] H_j: the checks use [3(x^2-1)] pk_i and [3(x^2-1)] g1 (k_scale_keys,
+  // G1_MGEN), e(S, H') e(-[m] pk, W) = (e(S, H) e(-pk, W))^m with m invertible mod r -- the same
+  // bit, without the last third of the cofactor clearing
+  if (hash_g2_group<HASH_K>(d, true, h, false)) G2pts[2 * j] = g2_to_affine(h);
 }
 #endif
 
@@ -735,8 +738,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_verify_wide(
     if (ct_job) {
       PA = U[j];
       PA.y = fq_neg(PA.y);
-      PB.x = fq_from_const(G1_GEN_X);
-      PB.y = fq_from_const(G1_GEN_Y);
+      PB.x = fq_from_const(G1_MGEN_X);  // [m] g1 against H' = [m] H
+      PB.y = fq_from_const(G1_MGEN_Y);
       PB.inf = false;
     } else {
       const size_t idx = (size_t)j * n + q;
@@ -843,8 +846,8 @@ __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict_
   if (q == n) {
     PA = U[j];
     PA.y = fq_neg(PA.y);
-    PB.x = fq_from_const(G1_GEN_X);
-    PB.y = fq_from_const(G1_GEN_Y);
+    PB.x = fq_from_const(G1_MGEN_X);  // [m] g1 against H' = [m] H
+    PB.y = fq_from_const(G1_MGEN_Y);
     PB.inf = false;
   } else {
     PA = S[(size_t)j * n + q];
@@ -858,6 +861,21 @@ __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict_
 #endif
 
 #if HBX_IN_TU(1)
+// pk_m[i] = [3(x^2-1)] pk_i (once per key set): the G1 side of the share checks against
+// H' = [3(x^2-1)] H (k_prepare_ct).
+__global__ void __launch_bounds__(64) k_scale_keys(const g1a* __restrict__ pk, uint32_t n, g1a* __restrict__ pk_m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  pk_m[i] = g1_to_affine(g1_mul_scalar(g1_from_affine(pk[i]), HEFF_M));
+}
+// H_j = hash_g1_g2(U_j, V_j) itself from H'_j = h_eff P (hbx_get_ct_hashes), compressed.
+__global__ void __launch_bounds__(64) k_true_hashes(const g2a* __restrict__ G2pts, uint32_t count,
+                                                    uint8_t* __restrict__ out96) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  g2_compress(g2_to_affine(g2_heff_to_h2(g2_from_affine(G2pts[2 * j]))), out96 + (size_t)j * 96);
+}
+
 // Shares of a ciphertext that failed Ciphertext::verify become HBX_SHARE_SKIPPED_CT: the
 // reference never verifies them (honey_badger.rs:371-376), so they are neither valid nor a fault.
 __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid, const uint8_t* __restrict__ ct_valid,

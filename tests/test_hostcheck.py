@@ -222,6 +222,29 @@ def test_g2_clear_cofactor_psi(hc):
         done += 1
 
 
+def test_heff_scaled_hash_point(hc):
+    """k_prepare_ct keeps Q = h_eff P = [3(x^2-1)] (h2 P) as H'; the checks scale their G1 side by
+    m = 3(x^2-1) (k_scale_keys, G1_MGEN) and hbx_get_ct_hashes maps Q back to h2 P."""
+    rnd = random.Random(12)
+    m = 3 * (0xD201000000010000 ** 2 - 1)
+    done = 0
+    while done < 2:
+        x = (rnd.randrange(bls.P), rnd.randrange(bls.P))
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is None:
+            continue
+        h = bls.g2_mul((x, y), bls.H2)
+        q96, h96 = ctypes.create_string_buffer(96), ctypes.create_string_buffer(96)
+        assert hc.hc_g2_heff(bls.g2_compress((x, y)), q96, h96) == 0
+        assert q96.raw == bls.g2_compress(bls.g2_mul(h, m))
+        assert h96.raw == bls.g2_compress(h)
+        done += 1
+    pk = bls.g1_mul(bls.G1_GEN, rnd.randrange(1, bls.R))
+    out = ctypes.create_string_buffer(48)
+    assert hc.hc_g1_scale_heff_m(bls.g1_compress(pk), out) == 0
+    assert out.raw == bls.g1_compress(bls.g1_mul(pk, m))
+
+
 def test_pairing_check_mixed_lines(hc):
     """Signature-share check shape: pair A over prepared lines, pair B's lines generated on the
     fly (un-normalised) from a varying G2 point."""

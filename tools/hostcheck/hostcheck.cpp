@@ -160,6 +160,18 @@ int hc_g1_mul_glv(const uint8_t* in48, const uint8_t* k32, uint8_t* out48) {
   g1j r = g1_add(g1_mul_u128_w4(p, k1), g1_mul_u128_w4(ph, k2));  // k_combine's windowed product
   g1_compress(g1_to_affine(r), out48); return 0;
 }
+// Q = h_eff P (k_prepare_ct's H') and back to h2 P (hbx_get_ct_hashes)
+int hc_g2_heff(const uint8_t* in96, uint8_t* q96, uint8_t* h96) {
+  g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
+  const g2j q = g2_heff(g2_from_affine(p));
+  g2_compress(g2_to_affine(q), q96);
+  g2_compress(g2_to_affine(g2_heff_to_h2(q)), h96);
+  return 0;
+}
+int hc_g1_scale_heff_m(const uint8_t* in48, uint8_t* out48) {
+  g1a p; if (g1_decompress(in48, p) != HBX_PT_OK) return -1;
+  g1_compress(g1_to_affine(g1_mul_scalar(g1_from_affine(p), HEFF_M)), out48); return 0;
+}
 int hc_g2_clear_cofactor(const uint8_t* in96, uint8_t* out96) {
   g2a p; if (g2_decompress(in96, p) != HBX_PT_OK) return -1;
   g2_compress(g2_to_affine(g2_clear_cofactor(g2_from_affine(p))), out96); return 0;
