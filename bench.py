@@ -53,15 +53,15 @@ MADS_PER_FQMUL = 288
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
 # rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_round.sh PMC=1,
-# profiles/r02i_pmc_hbm.txt, the digit-tower kernel of commit "Share check in a signed 28-bit
-# digit tower"): 5.058e6 KB + 8.544e6 KB per launch.  The accesses are the kernel's scratch
+# profiles/r02m_pmc_hbm.txt, the digit-tower kernel with the h_eff-scaled keys): 5.048e6 KB +
+# 8.592e6 KB per launch.  The accesses are the kernel's scratch
 # traffic (95 spilled VGPRs in the Miller loop, Fq12 operands of the out-of-line Fq12 products of
 # the final exponentiation), a width the guide leaves uncalibrated, so the raw counter bytes are
 # reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~12 MB
 # (shares 48 B + pk + 30 KB of digit-form lines per proposer + 1 B out): the kernel is VALU-bound
 # and the traffic (~0.56 TB/s) is not its bound.
-TRAFFIC_N256_BYTES = (5.058e6 + 8.544e6) * 1024
-TRAFFIC_SOURCE = "profiles/r02i_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
+TRAFFIC_N256_BYTES = (5.048e6 + 8.592e6) * 1024
+TRAFFIC_SOURCE = "profiles/r02m_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
 # The benchmarked node is validator 0: its own decryption shares are computed locally
 # (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
 OWN_INDEX = 0
