@@ -26,8 +26,8 @@ FaultyShareAdversary, tests/honey_badger.rs:99-106).  After the timed steps the 
 must equal "not corrupted" and every plaintext must equal its contribution, or the bench fails.
 
 Roofline: the dominant kernel is the share verification (k_verify_shares).  Its algorithmic work
-is 15,541 Fq multiplications per share (tools/opcount: 2-pair Miller loop 7,400 + final
-exponentiation 8,141; the 486 of the share's decode run in k_decompress_shares) x 288 32-bit
+is 15,057 Fq multiplications per share (tools/opcount: 2-pair Miller loop 7,400 + final
+exponentiation 7,657; the 486 of the share's decode run in k_prepare_ct / k_decompress_shares) x 288 32-bit
 multiply-adds each; its launch time is measured with HIP events recorded on the stream it runs on.  The bound is integer VALU (v_mad_u64_u32), not HBM
 or MFMA; the peak is the measured chip rate from tools/microbench.
 """
@@ -46,7 +46,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # Algorithmic work per unit (tools/opcount/opcount.cpp)
-FQMUL_PER_SHARE_VERIFY = 15541
+FQMUL_PER_SHARE_VERIFY = 15057  # opcount: miller_loop2 7400 + final_exp 7657 (decode excluded)
 MADS_PER_FQMUL = 288
 # Chip peak of 32x32->64-bit integer multiply-add (v_mad_u64_u32), measured by
 # tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.

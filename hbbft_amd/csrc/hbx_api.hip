@@ -94,7 +94,8 @@ struct hbx_ctx {
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
       coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
   // PublicKey::verify batches (hbx_verify_sigs)
-  dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
+  dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_lines_d, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
+  dbuf coin_lines_d;  // the nonces' lines in the coin check's digit form
   // SyncKeyGen commitment checks (hbx_bivar_rows / hbx_bivar_check_acks)
   dbuf bv_commit48, bv_C, bv_cst, bv_rows, bv_rows48, bv_pst, bv_ackp, bv_acky, bv_vals, bv_out;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
@@ -440,7 +441,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
-                  &c->vs_pk, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
+                  &c->vs_pk, &c->vs_lines_d, &c->coin_lines_d, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
                   &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
@@ -849,6 +850,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   hipStream_t s = c->stream;
   if (!c->coin_blob.ensure(total ? total : 16) || !c->coin_off.ensure((size_t)(count + 1) * 8) ||
       !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
+      !c->coin_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
       !c->coin_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->coin_out96.ensure((size_t)count * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
   if (total) HIPCHK(c, hipMemcpyAsync(c->coin_blob.p, nonce_blob, total, hipMemcpyHostToDevice, s));
@@ -867,7 +869,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                       c->coin_scratch.as<fq2>(), nl, nullptr);
+                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>());
   }
   HIPCHK(c, hipGetLastError());
   if (h96) {
@@ -922,7 +924,7 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_VERIFY_SIG, s);
-    hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
+    hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
                        c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
                        c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
                        c->coin_valid.as<uint8_t>());
@@ -949,6 +951,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   if (!c->vs_pk.ensure((size_t)count * 48) || !c->vs_blob.ensure(total ? total : 16) ||
       !c->vs_off.ensure((size_t)(count + 1) * 8) || !c->vs_H.ensure((size_t)count * sizeof(g2a)) ||
       !c->vs_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
+      !c->vs_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
       !c->vs_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->vs_sig96.ensure((size_t)count * 96) ||
       !c->vs_sig.ensure((size_t)count * sizeof(g2a)) || !c->vs_sig_st.ensure((size_t)count * 4) ||
       !c->vs_status.ensure(count))
@@ -970,12 +973,12 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   HIPCHK(c, hipGetLastError());
   const uint32_t nl = count * MILLER_LINES;
   hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->vs_lines.as<line_pre>(),
-                     c->vs_scratch.as<fq2>(), nl, nullptr);
+                     c->vs_scratch.as<fq2>(), nl, c->vs_lines_d.as<line_pre_d>());
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_VERIFY_SIG, s);
     hipLaunchKernelGGL(k_verify_sigs, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_pk.as<uint8_t>(),
-                       c->vs_lines.as<line_pre>(), c->vs_H.as<g2a>(), c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(),
+                       c->vs_lines_d.as<line_pre_d>(), c->vs_H.as<g2a>(), c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(),
                        count, c->vs_status.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());

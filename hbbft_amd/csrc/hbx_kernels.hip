@@ -916,6 +916,18 @@ __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict_
   out[i] = p;
 }
 
+// check_mixed in the signed-digit tower (pairingd.hpp): the same verdict; `slot` is this lane's
+// LDS slot for the final exponentiation's base.
+__device__ __forceinline__ bool check_mixed_d(const line_pre_d* LA, const g1a& PA, bool qa_inf, const g2a& QB,
+                                              const g1a& PB, lds_u32* slot) {
+  const bool skipA = PA.inf || qa_inf;
+  const bool skipB = PB.inf || QB.inf;
+  if (skipA && skipB) return true;
+  const fq12d f = miller_loop_mixed_d(LA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), !skipA, fq2d_from_fq2(QB.x),
+                                      fq2d_from_fq2(QB.y), fqd_from_fq(PB.x), fqd_from_fq(PB.y), !skipB);
+  return fq12d_is_one(final_exponentiation_d(f, slot));
+}
+
 // e(PA, QA) e(PB, QB) == 1 with QA prepared and QB's lines on the fly; pairings with the
 // identity contribute 1.
 __device__ __forceinline__ bool check_mixed(const line_pre* LA, const g1a& PA, bool qa_inf, const g2a& QB,
@@ -929,12 +941,13 @@ __device__ __forceinline__ bool check_mixed(const line_pre* LA, const g1a& PA, b
 
 // B1: PublicKeyShare::verify(share, nonce) (common_coin.rs:151): e(pk_i, H) == e(g1, sig_i),
 // i.e. e(pk_i, H) e(-g1, sig_i) == 1.  Lane = node i, blockIdx.y = coin instance.
-__global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __restrict__ lines, const g2a* __restrict__ H,
+__global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre_d* __restrict__ lines, const g2a* __restrict__ H,
                                                           const g1a* __restrict__ pk, uint32_t n_keys,
                                                           const g2a* __restrict__ sig,
                                                           const int32_t* __restrict__ sig_status,
                                                           const uint8_t* __restrict__ present, uint32_t n,
                                                           uint8_t* __restrict__ valid) {
+  __shared__ uint32_t gslots[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // final-exp base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t inst = blockIdx.y;
   if (i >= n) return;
@@ -946,7 +959,8 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __rest
     ng.x = fq_from_const(G1_GEN_X);
     ng.y = fq_neg(fq_from_const(G1_GEN_Y));
     ng.inf = false;
-    v = check_mixed(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng);
+    v = check_mixed_d(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng,
+                      (lds_u32*)(gslots + threadIdx.x));
   }
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
 }
@@ -958,10 +972,11 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre* __rest
 // lines differ per lane, so the mixed loop's plain loads).  The key is decoded here as pairing's
 // into_affine does (curve + G1 membership); an identity key or signature reduces the check to
 // "both are the identity" (e(O, H) = 1, and e(pk, H) = 1 only for pk = O since H != O).
-__global__ void __launch_bounds__(64) k_verify_sigs(const uint8_t* __restrict__ pk48, const line_pre* __restrict__ lines,
+__global__ void __launch_bounds__(64) k_verify_sigs(const uint8_t* __restrict__ pk48, const line_pre_d* __restrict__ lines,
                                                     const g2a* __restrict__ H, const g2a* __restrict__ sig,
                                                     const int32_t* __restrict__ sig_st, uint32_t count,
                                                     uint8_t* __restrict__ status) {
+  __shared__ uint32_t gslots[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // final-exp base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   g1a pk;
@@ -982,7 +997,7 @@ __global__ void __launch_bounds__(64) k_verify_sigs(const uint8_t* __restrict__ 
     ng.x = fq_from_const(G1_GEN_X);
     ng.y = fq_neg(fq_from_const(G1_GEN_Y));
     ng.inf = false;
-    v = check_mixed(lines + (size_t)i * MILLER_LINES, pk, H[i].inf, s, ng);
+    v = check_mixed_d(lines + (size_t)i * MILLER_LINES, pk, H[i].inf, s, ng, (lds_u32*)(gslots + threadIdx.x));
   }
   status[i] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
 }

@@ -37,6 +37,94 @@ HBX_HD fq12d miller_loop2_d(const line_pre_d* LA, const fqd& ax, const fqd& ay, 
   return fq12d_conj(f);
 }
 
+// ----------------------------------------------------------------------------------------------
+// Lines generated on the fly (a varying G2 point: the coin's signature shares, common_coin.rs:151)
+// -- pairing.hpp line_dbl_step / line_add_step / fq12_mul_by_014_f2 / miller_loop_mixed in the
+// digit tower.  Values that feed products are reduced (or are sums of two reduced values).  The
+// line steps and the Fq2-coefficient line product are out-of-line copies: inlined into the mixed
+// loop they made one function too large to compile in reasonable time.
+// ----------------------------------------------------------------------------------------------
+struct g2jd {
+  fq2d x, y, z;
+};
+// Raw line through the doubling of T, scaled by 2 Y Z^3: c0 = 3X^3 - 2Y^2, c1 = -3X^2 Z^2,
+// c2 = 2YZ^3;  T <- 2T.
+HBX_HDNI void line_dbl_step_d(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
+  const fq2d A = fq2d_sqr(T.x);
+  const fq2d B = fq2d_sqr(T.y);
+  const fq2d C = fq2d_sqr(B);
+  const fq2d ZZ = fq2d_sqr(T.z);
+  const fq2d E = fq2d_norm(fq2d_add(fq2d_dbl(A), A));
+  c0 = fq2d_reduce(fq2d_sub(fq2d_mul(E, T.x), fq2d_dbl(B)));
+  c1 = fq2d_neg(fq2d_mul(E, ZZ));
+  const fq2d D = fq2d_reduce(fq2d_dbl(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(T.x, B)), A), C)));
+  const fq2d F = fq2d_sqr(E);
+  const fq2d X3 = fq2d_reduce(fq2d_sub(F, fq2d_dbl(D)));
+  const fq2d C8 = fq2d_dbl(fq2d_reduce(fq2d_dbl(fq2d_dbl(C))));
+  const fq2d Y3 = fq2d_reduce(fq2d_sub(fq2d_mul(E, fq2d_sub(D, X3)), C8));
+  const fq2d Z3 = fq2d_reduce(fq2d_dbl(fq2d_mul(T.y, T.z)));
+  c2 = fq2d_mul(Z3, ZZ);
+  T = g2jd{X3, Y3, Z3};
+}
+// Raw line through T and the affine base point (qx, qy), scaled by den = Z (X - xQ Z^2):
+// c0 = num xQ - yQ den, c1 = -num, c2 = den;  T <- T + Q (madd-2007-bl).
+HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
+  const fq2d Z1Z1 = fq2d_sqr(T.z);
+  const fq2d U2 = fq2d_mul(qx, Z1Z1);
+  const fq2d S2 = fq2d_mul(fq2d_mul(qy, T.z), Z1Z1);
+  const fq2d H = fq2d_sub(U2, T.x);
+  const fq2d num = fq2d_sub(T.y, S2);
+  const fq2d den = fq2d_neg(fq2d_mul(T.z, H));
+  c0 = fq2d_reduce(fq2d_sub(fq2d_mul(num, qx), fq2d_mul(qy, den)));
+  c1 = fq2d_neg(num);
+  c2 = den;
+  const fq2d HH = fq2d_sqr(H);
+  const fq2d I = fq2d_reduce(fq2d_dbl(fq2d_dbl(HH)));
+  const fq2d J = fq2d_mul(H, I);
+  const fq2d r = fq2d_reduce(fq2d_dbl(fq2d_sub(S2, T.y)));
+  const fq2d V = fq2d_mul(T.x, I);
+  const fq2d X3 = fq2d_reduce(fq2d_sub(fq2d_sub(fq2d_sqr(r), J), fq2d_dbl(V)));
+  const fq2d Y3 = fq2d_reduce(fq2d_sub(fq2d_mul(r, fq2d_sub(V, X3)), fq2d_dbl(fq2d_mul(T.y, J))));
+  const fq2d Z3 = fq2d_reduce(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_norm(fq2d_add(T.z, H))), Z1Z1), HH));
+  T = g2jd{X3, Y3, Z3};
+}
+// f * (c0 + c1 v + c4 v w) with c4 in Fq2 (an un-normalised line at a G1 point)
+HBX_HDNI fq12d fq12d_mul_by_014_f2(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
+  const fq6d aa = fq6d_mul_by_01(f.c0, c0, c1);
+  const fq6d bb = fq6d{fq2d_mul_xi(fq2d_mul(f.c1.c2, c4)), fq2d_mul(f.c1.c0, c4), fq2d_mul(f.c1.c1, c4)};
+  const fq2d o = fq2d_norm(fq2d_add(c1, c4));
+  const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, o);
+  return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bb), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bb))};
+}
+// pairing.hpp miller_loop_mixed: pair A over prepared digit-form lines (plain loads: the lines may
+// differ per lane), pair B's lines generated from QB = (qx, qy) and evaluated un-normalised at PB.
+// One out-of-line copy (the coin and the PublicKey::verify kernels share it).
+HBX_HDNI fq12d miller_loop_mixed_d(const line_pre_d* LA, const fqd& ax, const fqd& ay, bool useA, const fq2d& qx,
+                                 const fq2d& qy, const fqd& bx, const fqd& by, bool useB) {
+  fq12d f = fq12d_one();
+  g2jd T{qx, qy, fq2d{fqd_const(FQD_ONE), fqd_zero()}};
+  int k = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12d_sqr(f);
+#pragma unroll 1
+    for (int s = 0; s < (((BLS_X >> i) & 1) ? 2 : 1); s++) {
+      if (useA) {
+        const line_pre_d L = LA[k];
+        f = fq12d_mul_by_014(f, L.c0, fq2d_mul_fq(L.c1, ax), ay);
+      }
+      if (useB) {
+        fq2d c0, c1, c2;
+        if (s == 0) line_dbl_step_d(T, c0, c1, c2);
+        else line_add_step_d(T, qx, qy, c0, c1, c2);
+        f = fq12d_mul_by_014_f2(f, c0, fq2d_mul_fq(c1, bx), fq2d_mul_fq(c2, by));
+      }
+      k++;
+    }
+  }
+  return fq12d_conj(f);
+}
+
 // Out-of-line copies (one each) for the final exponentiation's cold calls.
 HBX_HDNI fq12d fq12d_mul_ni(const fq12d& a, const fq12d& b) { return fq12d_mul(a, b); }
 HBX_HDNI fq12d fq12d_frobenius_ni(const fq12d& a) { return fq12d_frobenius(a); }

@@ -258,6 +258,21 @@ def test_pairing_check_mixed_lines(hc):
     assert hc.hc_pairing_check_mixed(pa, h, ng1, bad) == 0
 
 
+def test_digit_tower_mixed_check(hc):
+    """The coin share check in the digit tower (pairingd.hpp miller_loop_mixed_d: lines of the
+    signature share generated on the fly) equals pairing.hpp's element for element, valid and
+    invalid shares."""
+    rnd = random.Random(23)
+    for trial in range(3):
+        sk = rnd.randrange(1, bls.R)
+        h = bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R))
+        pk = bls.g1_compress(bls.g1_mul(bls.G1_GEN, sk))
+        sig = bls.g2_compress(bls.g2_mul(h, sk + (trial == 2)))
+        ng1 = bls.g1_compress(bls.g1_neg(bls.G1_GEN))
+        want = 1 if trial < 2 else 0
+        assert hc.hc_pairing_check_mixed_d(pk, bls.g2_compress(h), ng1, sig) == want + 6
+
+
 def test_g1_mul_glv(hc):
     """k_combine's two-lane GLV scalar multiplication (k1 P + k2 phi(P)) against the oracle."""
     rnd = random.Random(7)

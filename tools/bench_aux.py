@@ -72,6 +72,13 @@ def coin(ctx, steps):
     kms = k_ms / max(k_cnt, 1)
     return {"config": "C4 CommonCoin N=128 x 256 instances", "sig_share_verifies": inst * n,
             "verify_sig_kernel_ms": round(kms, 3), "sig_share_verifies_per_s_kernel": round(inst * n / (kms * 1e-3), 1),
+            # tools/opcount: mixed Miller loop 9,631 + final exponentiation 7,657 Fq-mul per check,
+            # 288 MAD each; peak 27.27 T MAD/s (tools/microbench/mad_rate.hip).  32,768 checks are
+            # 512 waves: half the SIMDs at one wave each.
+            "verify_sig_roofline": {"bound": "valu-int (v_mad_u64_u32)",
+                                    "achieved_Tmad_s": round(inst * n * 17288 * 288 / (kms * 1e-3) / 1e12, 3),
+                                    "peak_Tmad_s": 27.27,
+                                    "frac": round(inst * n * 17288 * 288 / (kms * 1e-3) / 1e12 / 27.27, 4)},
             "coin_round_ms_wall": round(sum(wall.values()), 3), "wall_ms": wall, "kernel_ms": kern,
             "note": "host API (PCIe staging of 3.1 MB of shares included in wall times)"}
 

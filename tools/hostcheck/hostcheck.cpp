@@ -145,6 +145,33 @@ int hc_pairing_check_mixed(const uint8_t* pa, const uint8_t* qa, const uint8_t* 
   g2_prepare_lines(QA, LA, scratch);
   return fq12_is_one(final_exponentiation(miller_loop_mixed(LA, PA, true, QB, PB, true))) ? 1 : 0;
 }
+// the coin check in the digit tower (miller_loop_mixed_d + final_exponentiation_d) against
+// pairing.hpp's: returns 1 + 2 (Miller output equal) + 4 (final exponentiation equal) when the
+// check holds, 0 + 2 + 4 when it does not; -1.. on a bad encoding
+int hc_pairing_check_mixed_d(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK) return -1;
+  if (g1_decompress(pb, PB) != HBX_PT_OK) return -2;
+  if (g2_decompress(qa, QA) != HBX_PT_OK) return -3;
+  if (g2_decompress(qb, QB) != HBX_PT_OK) return -4;
+  static line_pre LA[MILLER_LINES];
+  static line_pre_d DA[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  for (int i = 0; i < MILLER_LINES; i++) DA[i] = line_to_d(LA[i]);
+  const fq12 f = miller_loop_mixed(LA, PA, true, QB, PB, true);
+  const fq12d fd = miller_loop_mixed_d(DA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), true, fq2d_from_fq2(QB.x),
+                                       fq2d_from_fq2(QB.y), fqd_from_fq(PB.x), fqd_from_fq(PB.y), true);
+  const fq12 g = fq12d_to_fq12(fd);
+  static uint32_t slot[LDS_FQ12D_DWORDS];
+  const fq12 e1 = final_exponentiation(f);
+  const fq12 e2 = fq12d_to_fq12(final_exponentiation_d(fd, slot));
+  const fq* a = &f.c0.c0.c0; const fq* b = &g.c0.c0.c0;
+  const fq* x = &e1.c0.c0.c0; const fq* y = &e2.c0.c0.c0;
+  int same_m = 1, same_e = 1;
+  for (int i = 0; i < 12; i++) { same_m &= fq_eq(a[i], b[i]) ? 1 : 0; same_e &= fq_eq(x[i], y[i]) ? 1 : 0; }
+  return (fq12_is_one(e2) ? 1 : 0) + 2 * same_m + 4 * same_e;
+}
 // k * P (P compressed, k 32-byte big-endian canonical scalar) through the GLV split, as k_combine
 int hc_g1_mul_glv(const uint8_t* in48, const uint8_t* k32, uint8_t* out48) {
   g1a p; if (g1_decompress(in48, p) != HBX_PT_OK) return -1;

@@ -8,6 +8,7 @@ unsigned long long hbx_opcount_fqmul = 0;
 #include <cstdio>
 #include <cstring>
 #include "../../hbbft_amd/csrc/pairing.hpp"
+#include "../../hbbft_amd/csrc/pairingd.hpp"
 #include "../../hbbft_amd/csrc/hash.hpp"
 using namespace hbx;
 
@@ -47,9 +48,29 @@ int main() {
   hbx_opcount_fqmul = 0;
   g1_to_affine(g1_mul_scalar(g1_from_affine(P), k));
   const unsigned long long c_g1mul = hbx_opcount_fqmul;
+  // the share check as k_verify_shares runs it (digit tower; same algorithm, same count expected)
+  static line_pre_d D1[MILLER_LINES], D2[MILLER_LINES];
+  for (int i = 0; i < MILLER_LINES; i++) { D1[i] = line_to_d(L1[i]); D2[i] = line_to_d(L2[i]); }
+  const fqd px = fqd_from_fq(P.x), py = fqd_from_fq(P.y), ny = fqd_from_fq(nP.y);
+  hbx_opcount_fqmul = 0;
+  const fq12d fdd = miller_loop2_d(D1, px, py, true, D2, px, ny, true);
+  const unsigned long long c_miller_d = hbx_opcount_fqmul;
+  static uint32_t slot[LDS_FQ12D_DWORDS];
+  hbx_opcount_fqmul = 0;
+  (void)final_exponentiation_d(fdd, slot);
+  const unsigned long long c_fexp_d = hbx_opcount_fqmul;
+  fprintf(stderr, "digit tower: miller %llu final_exp %llu (conversions and inversion included)\n", c_miller_d, c_fexp_d);
+  // the coin's signature-share check: pair A over prepared lines, pair B's lines on the fly
+  hbx_opcount_fqmul = 0;
+  const fq12 fm = miller_loop_mixed(L1, P, true, Q, nP, true);
+  const unsigned long long c_mixed = hbx_opcount_fqmul;
+  hbx_opcount_fqmul = 0;
+  (void)fq12_is_one(final_exponentiation(fm));
+  const unsigned long long c_fexp2 = hbx_opcount_fqmul;
   printf("{\"check_ok\": %d, \"hash_g2\": %llu, \"prepare_lines\": %llu, \"miller_loop2\": %llu, "
          "\"final_exp\": %llu, \"g1_decompress\": %llu, \"g1_mul_255\": %llu, "
-         "\"verify_share\": %llu}\n",
-         ok ? 1 : 0, c_hash, c_lines, c_miller, c_fexp, c_dec, c_g1mul, c_dec + c_miller + c_fexp);
+         "\"verify_share\": %llu, \"miller_loop_mixed\": %llu, \"verify_sig_share\": %llu}\n",
+         ok ? 1 : 0, c_hash, c_lines, c_miller, c_fexp, c_dec, c_g1mul, c_dec + c_miller + c_fexp, c_mixed,
+         c_mixed + c_fexp2);
   return 0;
 }
