@@ -66,7 +66,7 @@ struct hbx_ctx {
   dbuf pk, pk_m, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk (k_scale_keys)
   // epoch state
   uint32_t p_ct = 0;
-  dbuf U, G2pts, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
+  dbuf U, G2pts, Hj, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
   // own-share mode (hbx_set_own_share): this node's index and secret share (8 LE limbs), and its
   // own decryption shares of the prepared ciphertexts
   uint32_t own_me = UINT32_MAX;
@@ -430,7 +430,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
-  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts,
+  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback,
@@ -551,7 +551,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
-  if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) ||
+  if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) || !c->Hj.ensure((size_t)p * sizeof(g2j)) ||
       !c->lines.ensure((size_t)p * sizeof(line_block)) || !c->lines_d.ensure((size_t)p * sizeof(line_block_d)) ||
       !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
       !c->ct_valid.ensure(p) || !c->dec_st.ensure((size_t)2 * p * 4))
@@ -580,7 +580,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
                                 : hash_blocks + dec_blocks + share_blocks;
       hipLaunchKernelGGL(k_prepare_ct, dim3(nb), b64, 0, s, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, hash_blocks,
                          c->U.as<g1a>(), c->G2pts.as<g2a>(), c->dec_st.as<int32_t>(),
-                         own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->digest,
+                         own ? c->own_sk.as<uint32_t>() : nullptr, own ? c->own_part.as<g1j>() : nullptr, c->Hj.as<g2j>(), c->digest,
                          b0, dec_blocks, early_shares, m_early, early_n ? early_n : 1u, me_early, c->S.as<g1a>(),
                          c->S_status.as<int32_t>());
     }
@@ -595,11 +595,13 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
                        own ? c->own_S.as<g1a>() : nullptr, early_n, me_early,
-                       own_entry ? c->S.as<g1a>() : nullptr, own_entry ? c->S_status.as<int32_t>() : nullptr);
+                       own_entry ? c->S.as<g1a>() : nullptr, own_entry ? c->S_status.as<int32_t>() : nullptr,
+                       c->Hj.as<g2j>());
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = 2 * p * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), b64, 0, s, c->lines.as<line_pre>(),
-                       c->scratch.as<fq2>(), nl, c->lines_d.as<line_pre_d>());
+                       c->scratch.as<fq2>(), nl, c->lines_d.as<line_pre_d>(), c->G2pts.as<g2a>(),
+                       c->Hj.as<g2j>());
   }
   HIPCHK(c, hipGetLastError());
   c->p_ct = p;
@@ -865,11 +867,11 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
                        c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
-                       UINT32_MAX, nullptr, nullptr);
+                       UINT32_MAX, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>());
+                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
   }
   HIPCHK(c, hipGetLastError());
   if (h96) {
@@ -969,11 +971,11 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
                      c->vs_lines.as<line_pre>(), c->vs_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
-                     UINT32_MAX, nullptr, nullptr);
+                     UINT32_MAX, nullptr, nullptr, nullptr);
   HIPCHK(c, hipGetLastError());
   const uint32_t nl = count * MILLER_LINES;
   hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->vs_lines.as<line_pre>(),
-                     c->vs_scratch.as<fq2>(), nl, c->vs_lines_d.as<line_pre_d>());
+                     c->vs_scratch.as<fq2>(), nl, c->vs_lines_d.as<line_pre_d>(), nullptr, nullptr);
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_VERIFY_SIG, s);
@@ -1195,9 +1197,9 @@ int hbx_get_ct_hashes(hbx_ctx* c, uint8_t* h96, size_t count) {
   HIPCHK(c, hipDeviceSynchronize());
   dbuf out;
   if (!out.ensure(count * 96)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_get_ct_hashes: out of device memory");
-  // G2pts holds H' = h_eff P = [3(x^2-1)] H (k_prepare_ct); the reference's H = h2 P from it
+  // Hj holds H' = h_eff P = [3(x^2-1)] H (k_prepare_ct); the reference's H = h2 P from it
   hipLaunchKernelGGL(k_true_hashes, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, c->stream, c->G2pts.as<g2a>(),
-                     (uint32_t)count, out.as<uint8_t>());
+                     c->Hj.as<g2j>(), (uint32_t)count, out.as<uint8_t>());
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) e = hipMemcpy(h96, out.p, count * 96, hipMemcpyDeviceToHost);

@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
                                                    uint32_t hash_blocks, g1a* __restrict__ U,
                                                    g2a* __restrict__ G2pts, int32_t* __restrict__ dec_st,
                                                    const uint32_t* __restrict__ own_sk, g1j* __restrict__ own_part,
-                                                   int digest, uint32_t block0, uint32_t dec_blocks,
+                                                   g2j* __restrict__ Hj, int digest, uint32_t block0, uint32_t dec_blocks,
                                                    const uint8_t* __restrict__ shares, size_t share_count,
                                                    uint32_t n, uint32_t me, g1a* __restrict__ S,
                                                    int32_t* __restrict__ S_status) {
@@ -169,7 +169,17 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
   // H'_j = h_eff P = [3(x^2-1)] H_j: the checks use [3(x^2-1)] pk_i and [3(x^2-1)] g1 (k_scale_keys,
   // G1_MGEN), e(S, H') e(-[m] pk, W) = (e(S, H) e(-pk, W))^m with m invertible mod r -- the same
   // bit, without the last third of the cofactor clearing
-  if (hash_g2_group<HASH_K>(d, true, h, false)) G2pts[2 * j] = g2_to_affine(h);
+  // kept in Jacobian form (Hj): the lines are made from (X, Y) on the isomorphic twist and
+  // corrected by Z in k_normalise_lines (g2_normalise_line_z), so no inversion sits on this chain;
+  // G2pts[2j] carries only the identity flag
+  if (hash_g2_group<HASH_K>(d, true, h, false)) {
+    Hj[j] = h;
+    g2a flag;
+    flag.x = fq2_zero();
+    flag.y = fq2_zero();
+    flag.inf = g2j_is_identity(h);
+    G2pts[2 * j] = flag;
+  }
 }
 #endif
 
@@ -269,7 +279,8 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
                                                       uint8_t* __restrict__ ct_ok, const g1j* __restrict__ own_part,
                                                       g1a* __restrict__ own_S, uint32_t n, uint32_t me,
-                                                      g1a* __restrict__ S, int32_t* __restrict__ S_status) {
+                                                      g1a* __restrict__ S, int32_t* __restrict__ S_status,
+                                                      const g2j* __restrict__ Hj) {
   const uint32_t line_blocks = (count * LINE_K + 63) / 64;
   if (blockIdx.x >= line_blocks) {
     // own share S_j,me = k1 U_j + k2 phi(U_j) (k_prepare_ct's two halves) where U_j decoded
@@ -293,6 +304,10 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
   const int gbase = (int)(threadIdx.x & 63) - gl;
   if (k >= count) return;  // whole groups (LINE_K | 64)
   g2a q = pts[k];
+  if (Hj && (k & 1) == 0) {  // (X, Y) of the Jacobian hash point; Z enters in k_normalise_lines
+    q.x = Hj[k >> 1].x;
+    q.y = Hj[k >> 1].y;
+  }
   if (dec_st) {
     const uint32_t j = k >> 1;
     const int32_t su = dec_st[j], sw = dec_st[p + j];
@@ -326,11 +341,17 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
 // 68 T steps only, and this launch is 68x wider and one inversion deep.
 __global__ void __launch_bounds__(64) k_normalise_lines(line_pre* __restrict__ lines,
                                                         const fq2* __restrict__ c2, uint32_t count,
-                                                        line_pre_d* __restrict__ lines_d) {
+                                                        line_pre_d* __restrict__ lines_d,
+                                                        const g2a* __restrict__ pts, const g2j* __restrict__ Hj) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
   line_pre l = lines[k];
-  g2_normalise_line(l, c2[k]);
+  const uint32_t pt = k / MILLER_LINES;
+  // lines of a Jacobian hash point (k_prepare_lines with Hj) unless it was replaced by the
+  // identity; z = 1 otherwise (one code path for the wave: a branch would run both inversions)
+  fq2 z = fq2_one();
+  if (Hj && (pt & 1) == 0 && !pts[pt].inf) z = Hj[pt >> 1].z;
+  g2_normalise_line_z(l, c2[k], z);
   lines[k] = l;
   if (lines_d) lines_d[k] = line_to_d(l);
 }
@@ -869,11 +890,12 @@ __global__ void __launch_bounds__(64) k_scale_keys(const g1a* __restrict__ pk, u
   pk_m[i] = g1_to_affine(g1_mul_scalar(g1_from_affine(pk[i]), HEFF_M));
 }
 // H_j = hash_g1_g2(U_j, V_j) itself from H'_j = h_eff P (hbx_get_ct_hashes), compressed.
-__global__ void __launch_bounds__(64) k_true_hashes(const g2a* __restrict__ G2pts, uint32_t count,
-                                                    uint8_t* __restrict__ out96) {
+__global__ void __launch_bounds__(64) k_true_hashes(const g2a* __restrict__ G2pts, const g2j* __restrict__ Hj,
+                                                    uint32_t count, uint8_t* __restrict__ out96) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= count) return;
-  g2_compress(g2_to_affine(g2_heff_to_h2(g2_from_affine(G2pts[2 * j]))), out96 + (size_t)j * 96);
+  const g2j q = G2pts[2 * j].inf ? g2_identity() : Hj[j];
+  g2_compress(g2_to_affine(g2_heff_to_h2(q)), out96 + (size_t)j * 96);
 }
 
 // Shares of a ciphertext that failed Ciphertext::verify become HBX_SHARE_SKIPPED_CT: the

@@ -94,6 +94,18 @@ HBX_HD void g2_normalise_line(line_pre& l, const fq2& c2) {
   l.c1 = fq2_mul(l.c1, inv);
 }
 
+// g2_normalise_line for lines made from (X, Y) of a Jacobian point (X, Y, Z) taken as affine: that
+// is the point's image on the isomorphic twist y^2 = x^3 + b' Z^6 under (x, y) -> (Z^2 x, Z^3 y),
+// and the doubling / addition steps do not involve b'.  Its lines carry c0' = Z^3 c0, c1' = Z c1,
+// c2' = c2, so c0 = c0' / (c2' Z^3) and c1 = c1' Z^2 / (c2' Z^3): the line preparation needs no
+// inversion of Z (k_prepare_ct's hash point).
+HBX_HD void g2_normalise_line_z(line_pre& l, const fq2& c2, const fq2& z) {
+  const fq2 z2 = fq2_sqr(z);
+  const fq2 inv = fq2_inv(fq2_mul(c2, fq2_mul(z2, z)));
+  l.c0 = fq2_mul(l.c0, inv);
+  l.c1 = fq2_mul(fq2_mul(l.c1, z2), inv);
+}
+
 // Prepare the 68 normalised lines of Q (affine, not infinity) in one lane (host tools).
 // `scratch` holds 2*68 Fq2 of workspace (raw c2 values and their prefix products for one
 // batched inversion).

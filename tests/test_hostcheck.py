@@ -245,6 +245,19 @@ def test_heff_scaled_hash_point(hc):
     assert out.raw == bls.g1_compress(bls.g1_mul(pk, m))
 
 
+def test_lines_from_jacobian_point(hc):
+    """k_prepare_lines makes H's lines from (X, Y) of its Jacobian form (a point of the isomorphic
+    twist; no inversion in k_prepare_ct) and k_normalise_lines corrects them by Z: the 68 lines
+    equal the affine point's, for any representative z."""
+    rnd = random.Random(13)
+    for s in (3, 0x1234567, bls.R - 5):
+        q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, s))
+        z0, z1 = rnd.randrange(1, bls.P), rnd.randrange(bls.P)
+        assert hc.hc_lines_jac_cmp(q, z0.to_bytes(48, "big"), z1.to_bytes(48, "big")) == 0
+    # z = 1 is the affine case itself
+    assert hc.hc_lines_jac_cmp(bls.g2_compress(bls.G2_GEN), (1).to_bytes(48, "big"), bytes(48)) == 0
+
+
 def test_pairing_check_mixed_lines(hc):
     """Signature-share check shape: pair A over prepared lines, pair B's lines generated on the
     fly (un-normalised) from a varying G2 point."""

@@ -195,6 +195,26 @@ int hc_g2_heff(const uint8_t* in96, uint8_t* q96, uint8_t* h96) {
   g2_compress(g2_to_affine(g2_heff_to_h2(q)), h96);
   return 0;
 }
+// Lines of Q from (X, Y) of its Jacobian form (x z^2, y z^3, z) taken as affine, corrected by z in
+// the normalisation (k_prepare_lines + k_normalise_lines on k_prepare_ct's H'), against the affine
+// point's lines: returns the number of differing lines (0 = identical)
+int hc_lines_jac_cmp(const uint8_t* in96, const uint8_t* z0_48, const uint8_t* z1_48) {
+  g2a q; if (g2_decompress(in96, q) != HBX_PT_OK || q.inf) return -1;
+  fq2 z; z.c0 = fq_from_be(z0_48); z.c1 = fq_from_be(z1_48);
+  const fq2 zz = fq2_sqr(z);
+  g2a qz = q; qz.x = fq2_mul(q.x, zz); qz.y = fq2_mul(q.y, fq2_mul(zz, z));
+  static line_pre a[MILLER_LINES], b[MILLER_LINES];
+  static fq2 ca[MILLER_LINES], cb[MILLER_LINES];
+  g2_raw_lines(q, a, ca);
+  g2_raw_lines(qz, b, cb);
+  int bad = 0;
+  for (int i = 0; i < MILLER_LINES; i++) {
+    g2_normalise_line(a[i], ca[i]);
+    g2_normalise_line_z(b[i], cb[i], z);
+    if (!fq2_eq(a[i].c0, b[i].c0) || !fq2_eq(a[i].c1, b[i].c1)) bad++;
+  }
+  return bad;
+}
 int hc_g1_scale_heff_m(const uint8_t* in48, uint8_t* out48) {
   g1a p; if (g1_decompress(in48, p) != HBX_PT_OK) return -1;
   g1_compress(g1_to_affine(g1_mul_scalar(g1_from_affine(p), HEFF_M)), out48); return 0;
