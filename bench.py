@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 3),
                     help="lanes per decryption-share check (0: auto by occupancy)")
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="also time this many consecutive epochs in flight at once (one context and stream "
+                         "each, as HoneyBadger's max_future_epochs allows); reported beside the headline")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
@@ -205,6 +208,50 @@ def cpu_baseline(ep, seconds: float, threads: int):
                        f"loop + one final exponentiation per share, {cols} whole proposer columns of the N={n} "
                        f"epoch in {db:.1f} s; (a) the reference's per-share shape {na / da:.0f}/s; a restatement, "
                        f"not the reference binary (no Rust toolchain)")
+
+
+def in_flight(args, ep, dev, torch, Context, inputs, pj, maxv, n, t, off, verifies):
+    """Throughput with `args.in_flight` consecutive epochs overlapping: epoch k on context k mod F
+    (own buffers and stream), issued back to back, so one epoch's latency-bound stages (hash-to-G2,
+    lines, combine) run beside another's share checks.  The headline `value` stays one epoch at a
+    time; this is the node's rate when future-epoch messages are already queued."""
+    F = args.in_flight
+    d_u, d_v, d_off, d_w, d_shares = inputs
+    lanes = []
+    for _ in range(F):
+        c = Context(dev.index or 0)
+        c.set_verify_lanes(args.verify_lanes)
+        assert (c.set_pk_shares([row.tobytes() for row in ep["pk_shares"]]) == 0).all()
+        if not args.no_own_share:
+            c.set_own_share(OWN_INDEX, ep["own_sk"])
+        st = torch.cuda.Stream(dev)
+        outs = (torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev), torch.zeros(pj * n, dtype=torch.uint8, device=dev),
+                torch.zeros(pj, dtype=torch.uint8, device=dev), torch.zeros(pj, dtype=torch.int32, device=dev))
+        lanes.append((c, st, outs))
+    torch.cuda.synchronize(dev)
+
+    def issue(k):
+        c, st, (o, v, cv, stt) = lanes[k % F]
+        c.decrypt_epoch_d(d_u, d_v, d_off, d_w, pj, maxv, d_shares, n, t, o, d_valid=v, d_ct_valid=cv, d_status=stt,
+                          stream=st.cuda_stream)
+
+    for k in range(F):
+        issue(k)
+    torch.cuda.synchronize(dev)
+    epochs = F * max(args.steps, 2)
+    t0 = time.perf_counter()
+    for k in range(epochs):
+        issue(k)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    for c, _, (o, v, cv, stt) in lanes:
+        assert (stt.cpu().numpy() == 0).all() and (cv.cpu().numpy() == 1).all(), "in-flight epoch status"
+        assert ((v.cpu().numpy().reshape(pj, n) == 1) == ~ep["corrupt"]).all(), "in-flight validity"
+        out = o.cpu().numpy()
+        assert all(out[off[j]:off[j + 1]].tobytes() == ep["msgs"][j] for j in range(pj)), "in-flight plaintexts"
+        c.close()
+    return {"epochs": epochs, "in_flight": F, "ms_per_epoch": round(elapsed / epochs * 1e3, 3),
+            "value": round(verifies * epochs / elapsed, 1), "unit": "share verifies/s"}
 
 
 def main():
@@ -359,6 +406,9 @@ def main():
                      "work": f"{shares_here} shares x {FQMUL_PER_SHARE_VERIFY} Fq-mul x {MADS_PER_FQMUL} MAD"},
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
     }
+    if world == 1 and args.in_flight > 1:
+        res["epochs_in_flight"] = in_flight(args, ep, dev, torch, Context, (d_u, d_v, d_off, d_w, d_shares), pj, maxv,
+                                            n, t, off, verifies)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(ep, args.cpu_seconds, min(16, os.cpu_count() or 1))
     if rank == 0:

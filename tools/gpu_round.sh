@@ -15,14 +15,14 @@ cat gpurun_out/${tag}_bench_shard8.json
 if [ "${PROF:-1}" = "1" ]; then
   R="$GRAFT_REPO_ROOT"
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${tag}_prof" -o run -- python3 -u "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/${tag}_prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${tag}_prof.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${tag}_prof" -o run -- python3 -u "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --in-flight 1 > "$R/gpurun_out/${tag}_prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${tag}_prof.log"; exit 1; }
   python3 "$R/tools/kstats.py" "$R/gpurun_out/${tag}_prof/run_results.db" > "$R/gpurun_out/${tag}_kernel_stats.txt" && cat "$R/gpurun_out/${tag}_kernel_stats.txt"
 fi
 if [ "${PMC:-0}" = "1" ]; then
   # HBM bytes of one N=256 epoch step: FETCH_SIZE and WRITE_SIZE in separate passes
   R="$GRAFT_REPO_ROOT"
   cd /tmp
-  B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+  B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --in-flight 1"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/${tag}_pf" -o run -- python3 -u $B > "$R/gpurun_out/${tag}_pf.log" 2>&1 || { echo "pmc fetch failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/${tag}_pw" -o run -- python3 -u $B > "$R/gpurun_out/${tag}_pw.log" 2>&1 || { echo "pmc write failed"; exit 1; }
   python3 "$R/tools/pmcsum.py" "$R/gpurun_out/${tag}_pf/run_results.db" "$R/gpurun_out/${tag}_pw/run_results.db" > "$R/gpurun_out/${tag}_pmc_hbm.txt" 2>&1 || true
