@@ -130,6 +130,52 @@ def test_own_share_mode_matches_golden(hbx_ctx, name):
 
 
 @pytest.mark.gpu
+def test_epochs_in_flight_on_two_contexts():
+    """Two epochs in flight (bench.py epochs_in_flight; HoneyBadger handles up to max_future_epochs
+    at once): one context and stream each, issued back to back without synchronising in between.
+    Contexts share nothing, so each epoch's statuses and plaintexts are those of the fixture."""
+    import torch
+
+    from hbbft_amd.hbx import Context
+
+    dev = torch.device("cuda", 0)
+    ds = [_load("hb_epoch_n64"), _load("hb_epoch_n7")]
+    ctxs = [Context(0), Context(0)]
+    try:
+        runs = []
+        for ctx, d in zip(ctxs, ds):
+            _set_keys(ctx, d)
+            p, n = d["shares"].shape[:2]
+            off = d["v_off"].astype(np.int64)
+            up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+            t = dict(u=up(d["u"]), w=up(d["w"]), v=up(d["v_blob"].copy() if len(d["v_blob"]) else np.zeros(1, np.uint8)),
+                     off=up(off), sh=up(d["shares"]), pr=up(d["present"].astype(np.uint8)),
+                     out=torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev),
+                     valid=torch.zeros(p * n, dtype=torch.uint8, device=dev),
+                     ct=torch.zeros(p, dtype=torch.uint8, device=dev), st=torch.zeros(p, dtype=torch.int32, device=dev))
+            runs.append((ctx, d, t, p, n, off, torch.cuda.Stream(dev)))
+        torch.cuda.synchronize(dev)
+        for _ in range(3):  # repeated, so later epochs overlap earlier ones on the other stream
+            for ctx, d, t, p, n, off, st in runs:
+                ctx.decrypt_epoch_d(t["u"], t["v"], t["off"], t["w"], p, int(np.max(np.diff(off))), t["sh"], n,
+                                    int(d["t"]), t["out"], d_valid=t["valid"], d_ct_valid=t["ct"], d_status=t["st"],
+                                    d_present=t["pr"], stream=st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        for ctx, d, t, p, n, off, st in runs:
+            np.testing.assert_array_equal(t["ct"].cpu().numpy(), d["expect_ct_status"])
+            np.testing.assert_array_equal(t["valid"].cpu().numpy().reshape(p, n), d["expect_share_status"])
+            status = t["st"].cpu().numpy()
+            np.testing.assert_array_equal(status, d["expect_status"])
+            out = t["out"].cpu().numpy()
+            for j in range(p):
+                if status[j] == 0:
+                    _check_plain(d, j, out[off[j]:off[j + 1]].tobytes())
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+
+
+@pytest.mark.gpu
 def test_unknown_sender_status(hbx_ctx):
     """Senders >= n of hbx_set_pk_shares: HBX_SHARE_UNKNOWN_SENDER (the reference returns
     Err(UnknownSender), honey_badger.rs:64-66), never a verification."""
