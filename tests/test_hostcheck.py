@@ -245,6 +245,22 @@ def test_heff_scaled_hash_point(hc):
     assert out.raw == bls.g1_compress(bls.g1_mul(pk, m))
 
 
+def test_binv_divsteps(hc):
+    """binv_limbs (batched Bernstein-Yang divsteps, every inversion of the kernels) against
+    Python's modular inverse, mod p and mod r, on random and edge values (0 -> 0)."""
+    rnd = random.Random(14)
+    for mod, nl, which in ((bls.P, 12, 0), (bls.R, 8, 1)):
+        vals = [0, 1, 2, 3, mod - 1, mod - 2, (mod + 1) // 2, 1 << 31, (1 << (32 * nl - 4)) % mod]
+        vals += [rnd.randrange(mod) for _ in range(300)]
+        vals += [rnd.randrange(1 << rnd.randrange(1, 40)) for _ in range(50)]  # short values
+        for x in vals:
+            xa = (ctypes.c_uint32 * nl)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(nl)])
+            out = (ctypes.c_uint32 * nl)()
+            hc.hc_binv(xa, which, out)
+            got = sum(int(out[i]) << (32 * i) for i in range(nl))
+            assert got == (pow(x, -1, mod) if x else 0), (which, x)
+
+
 def test_lines_from_jacobian_point(hc):
     """k_prepare_lines makes H's lines from (X, Y) of its Jacobian form (a point of the isomorphic
     twist; no inversion in k_prepare_ct) and k_normalise_lines corrects them by Z: the 68 lines

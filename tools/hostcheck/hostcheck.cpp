@@ -215,6 +215,13 @@ int hc_lines_jac_cmp(const uint8_t* in96, const uint8_t* z0_48, const uint8_t* z
   }
   return bad;
 }
+// binv_limbs (batched divsteps) on canonical little-endian limbs: which = 0 mod p (12 limbs),
+// 1 mod r (8 limbs)
+int hc_binv(const uint32_t* x, int which, uint32_t* out) {
+  if (which == 0) binv_limbs<12>(x, FQ_P, out);
+  else binv_limbs<8>(x, FR_R, out);
+  return 0;
+}
 int hc_g1_scale_heff_m(const uint8_t* in48, uint8_t* out48) {
   g1a p; if (g1_decompress(in48, p) != HBX_PT_OK) return -1;
   g1_compress(g1_to_affine(g1_mul_scalar(g1_from_affine(p), HEFF_M)), out48); return 0;
