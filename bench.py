@@ -60,8 +60,8 @@ PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 # reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~12 MB
 # (shares 48 B + pk + 30 KB of digit-form lines per proposer + 1 B out): the kernel is VALU-bound
 # and the traffic (~0.56 TB/s) is not its bound.
-TRAFFIC_N256_BYTES = (5.077e6 + 8.594e6) * 1024
-TRAFFIC_SOURCE = "profiles/r02v_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
+TRAFFIC_N256_BYTES = (5.069e6 + 8.579e6) * 1024
+TRAFFIC_SOURCE = "profiles/r02y_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
 # The benchmarked node is validator 0: its own decryption shares are computed locally
 # (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
 OWN_INDEX = 0
