@@ -168,11 +168,16 @@ HBX_HDNI g1j g1_mul_u128_w4(const g1a& P, const uint32_t* k4) {
 #pragma unroll 1
   for (int i = 2; i < 16; i++) tab[i] = g1_add_mixed_i(tab[i - 1], P);
   g1j acc = tab[k4[3] >> 28];
+  // the next window's table entry is loaded before this window's doublings, so the scratch read
+  // lands while they run
+  g1j nxt = tab[(k4[3] >> 24) & 0xFu];
 #pragma unroll 1
   for (int w = 30; w >= 0; w--) {
+    const g1j cur = nxt;
+    if (w > 0) nxt = tab[(k4[(w - 1) >> 3] >> (((w - 1) & 7) * 4)) & 0xFu];
 #pragma unroll 1
     for (int q = 0; q < 4; q++) acc = g1_dbl_i(acc);  // one inlined copy each: acc stays in VGPRs
-    acc = g1_add_i(acc, tab[(k4[w >> 3] >> ((w & 7) * 4)) & 0xFu]);
+    acc = g1_add_i(acc, cur);
   }
   return acc;
 }
