@@ -1,6 +1,8 @@
-"""Benchmark: one HoneyBadger node-epoch of threshold-decryption crypto at N=256 on MI355X.
+"""Benchmark: one HoneyBadger node-epoch of threshold-decryption crypto at N=256 on MI355X, plus the
+other BASELINE.json configs as sub-objects of the same JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--vlen 1024] [--no-cpu-baseline]
+                    [--configs C2,C4,C5]
 
 A *step* is the crypto of one HoneyBadger epoch as one node sees it (SURVEY.md §3 stack A,
 BASELINE.json configs[2]): for every one of the N accepted proposals
@@ -9,6 +11,10 @@ BASELINE.json configs[2]): for every one of the N accepted proposals
   * ``PublicKeySet::decrypt`` with the first f+1 valid shares      (honey_badger.rs:340),
 i.e. 65,536 share verifications + 256 ciphertext checks + 256 Lagrange combines (t = 86) + the
 hash_bytes keystream XOR, through the C ABI of libhbx.so on device-resident inputs.
+
+``configs`` (single GPU, rank 0 only): C2 (an N=64 epoch, BASELINE config 1), C4 (Common Coin,
+256 instances at N=128, config 3) and C5 (Broadcast, 128 x 1 MiB proposals at N=128, both Merkle
+digests, config 4), each with its own value, roofline and CPU baseline.
 
 Multi-GPU (``torchrun``), two modes:
   * ``--scaling strong`` (default; BASELINE config 3): ONE N=256 epoch sharded by proposer column
@@ -25,19 +31,22 @@ contributions; U/V/W made by ``hbx_encrypt`` and shares by ``hbx_decrypt_shares`
 FaultyShareAdversary, tests/honey_badger.rs:99-106).  After the timed steps the validity matrix
 must equal "not corrupted" and every plaintext must equal its contribution, or the bench fails.
 
-Roofline: the dominant kernel is the share verification (k_verify_shares).  Its algorithmic work
-is 15,057 Fq multiplications per share (tools/opcount: 2-pair Miller loop 7,400 + final
-exponentiation 7,657; the 486 of the share's decode run in k_prepare_ct / k_decompress_shares) x 288 32-bit
-multiply-adds each; its launch time is measured with HIP events recorded on the stream it runs on.  The bound is integer VALU (v_mad_u64_u32), not HBM
-or MFMA; the peak is the measured chip rate from tools/microbench.
+Roofline: the dominant kernel is the share verification (k_verify_shares / k_verify_shares2).  Its
+algorithmic work is FROZEN at SURVEY.md §8(d)'s unit V_dec = 16,500 Fq multiplications per share
+(2 precomputed-line Miller loops + 1 cyclotomic final exponentiation + 1 inversion) x 288 32-bit
+multiply-adds each; the current code's own count (tools/opcount) is reported beside it.  Its launch
+time is measured with HIP events recorded on the stream it runs on.  The bound is integer VALU
+(v_mad_u64_u32), not HBM or MFMA; the peak is the measured chip rate.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -45,26 +54,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Algorithmic work per unit (tools/opcount/opcount.cpp)
-FQMUL_PER_SHARE_VERIFY = 15057  # opcount: miller_loop2 7400 + final_exp 7657 (decode excluded)
-MADS_PER_FQMUL = 288
+# Frozen algorithmic work units (DESIGN.md §4 "Work units")
+VDEC_FQMUL = 16500     # one decryption-share verify
+VSIG_FQMUL = 20000     # one coin signature-share verify (sigma's lines generated in the loop)
+G1_MUL_FQMUL = 4100    # one G1 double-and-add scalar multiplication (C_t = t x 4.1k)
+MADS_PER_FQMUL = 288   # 2 x 12^2 (32-bit schoolbook Montgomery product)
+# Current code's own count (tools/opcount/opcount.cpp over the kernels' code), reported beside
+OPCOUNT_VDEC = 15057   # two-pair Miller loop 7,400 + final exponentiation 7,657
+OPCOUNT_VSIG = 17288   # mixed Miller loop 9,631 + final exponentiation 7,657
 # Chip peak of 32x32->64-bit integer multiply-add (v_mad_u64_u32), measured by
 # tools/microbench/mad_rate.hip on MI355X (profiles/r01_mad_rate.txt): tera-MAD/s.
 PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
-# HBM traffic of one k_verify_shares launch at N=256 (all 256 proposers on one GPU), from
-# rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes (tools/gpu_round.sh PMC=1,
-# profiles/r02m_pmc_hbm.txt, the digit-tower kernel with the h_eff-scaled keys): 5.048e6 KB +
-# 8.592e6 KB per launch.  The accesses are the kernel's scratch
-# traffic (95 spilled VGPRs in the Miller loop, Fq12 operands of the out-of-line Fq12 products of
-# the final exponentiation), a width the guide leaves uncalibrated, so the raw counter bytes are
-# reported without the x2 streaming-read correction.  Algorithmic bytes per launch are ~12 MB
-# (shares 48 B + pk + 30 KB of digit-form lines per proposer + 1 B out): the kernel is VALU-bound
-# and the traffic (~0.56 TB/s) is not its bound.
-TRAFFIC_N256_BYTES = (5.069e6 + 8.579e6) * 1024
-TRAFFIC_SOURCE = "profiles/r02y_pmc_hbm.txt (PMC FETCH_SIZE+WRITE_SIZE, digit-tower kernel)"
-# The benchmarked node is validator 0: its own decryption shares are computed locally
-# (hbx_set_own_share), and its own share's check doubles as Ciphertext::verify.
-OWN_INDEX = 0
+# 32-bit VALU lane-op peak (256 CUs x 4 SIMD x 16 lanes x 2.4 GHz) for the byte kernels
+PEAK_VALU_OPS = 256 * 4 * 16 * 2.4e9
+HBM_PEAK_GBPS = 8000.0
+# HBM traffic of one share-check launch at N=256, from a PMC pass (rocprofv3 --pmc FETCH_SIZE and
+# WRITE_SIZE in separate passes, tools/gpu_round.sh PMC=1): the newest profiles/*_pmc_hbm.json
+# carries the kernel, the bytes per launch and the commit the pass was taken at.
+OWN_INDEX = 0  # the benchmarked node is validator 0 (own share computed locally, hbx_set_own_share)
 
 
 def parse():
@@ -79,8 +86,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-own-share", action="store_true",
                     help="run Ciphertext::verify as separate checks instead of through the node's own share")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 3),
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per config")
+    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3),
                     help="lanes per decryption-share check (0: auto by occupancy)")
     ap.add_argument("--in-flight", type=int, default=2,
                     help="also time this many consecutive epochs in flight at once (one context and stream "
@@ -88,9 +95,63 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
+    ap.add_argument("--configs", default="C2,C4,C5",
+                    help="secondary BASELINE configs in the same line (single GPU only; '' for none)")
     return ap.parse_args()
 
 
+def host_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "affinity": usable}
+
+
+def all_cores() -> int:
+    """Row (b) threads: every host core, os.cpu_count()."""
+    return max(1, os.cpu_count() or 1)
+
+
+def traffic_record():
+    """Newest PMC record for the share check (profiles/*_pmc_hbm.json), or None."""
+    import glob
+
+    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_hbm.json")))
+    if not recs:
+        return None
+    with open(recs[-1]) as fh:
+        rec = json.load(fh)
+    rec["source"] = os.path.relpath(recs[-1], ROOT)
+    return rec
+
+
+def cpu_lib():
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_port.so"))
+    P, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    lib.cpu_verify_dec_shares.argtypes = [P, u32, P, P, P, P, P, P, u32, i32, P]
+    lib.cpu_verify_dec_shares_fused.argtypes = [P, u32, P, P, P, P, P, u32, P, u32, i32, P]
+    lib.cpu_verify_sig_shares.argtypes = [P, u32, P, P, u32, P, P, u32, i32, i32, P]
+    lib.cpu_combine_sigs.argtypes = [P, P, u32, u32, u32, P, P, P, i32, P, P]
+    lib.cpu_rs_encode.argtypes = [P, u32, u32, u32, u32, i32]
+    lib.cpu_rs_reconstruct.argtypes = [P, P, u32, u32, u32, u32, i32, P]
+    return lib
+
+
+# ----------------------------------------------------------------------------------------------
+# Stack A: HoneyBadger threshold decryption (C2, C3)
+# ----------------------------------------------------------------------------------------------
 def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
     """Synthetic inputs of proposers [lo, hi) of one epoch, built on the GPU (hbx producer API)."""
     from hbbft_amd import netinfo
@@ -120,36 +181,18 @@ def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
                 own_sk=sk_shares[OWN_INDEX].tobytes())
 
 
-def host_info():
-    model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as fh:
-            for line in fh:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"model": model, "nproc": os.cpu_count()}
-
-
-def cpu_baseline(ep, seconds: float, threads: int):
-    """CPU baseline ("port", tools/cpu_baseline/cpu_port.cpp, g++ -O3), both rows of BASELINE.md §2
-    on `threads` std::threads over a bounded sample of this workload's shares, each checked against
-    the expected bits:
-      (a) reference shape (honey_badger.rs:229 as threshold_crypto runs it): hash_g1_g2 recomputed
-          per share with pairing 0.14's 507-bit cofactor multiplication, two full pairings with
-          separate final exponentiations;
-      (b) hoisted + fused: hash_g1_g2 and the Miller lines of H_j, W_j once per proposer, then one
-          two-pair Miller loop and ONE final exponentiation per share.
-    `value` is row (b), the faster CPU formulation."""
-    import ctypes
-
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_port.so"))
-    P = ctypes.c_void_p
-    lib.cpu_verify_dec_shares.argtypes = [P, ctypes.c_uint32, P, P, P, P, P, P, ctypes.c_uint32, ctypes.c_int, P]
-    lib.cpu_verify_dec_shares_fused.argtypes = [P, ctypes.c_uint32, P, P, P, P, P, ctypes.c_uint32, P,
-                                                ctypes.c_uint32, ctypes.c_int, P]
+def cpu_baseline_dec(ep, seconds: float):
+    """CPU baseline ("port", tools/cpu_baseline/cpu_port.cpp, g++ -O3) of the decryption-share
+    checks, both rows of BASELINE.md §2 over a bounded sample of this workload's shares, each
+    checked against the expected bits:
+      (a) 1 thread, the reference's shape (honey_badger.rs:229 as threshold_crypto runs it):
+          hash_g1_g2 recomputed per share with pairing 0.14's 507-bit cofactor multiplication, two
+          full pairings with separate final exponentiations;
+      (b) all host cores (os.cpu_count() std::threads), hoisted + fused: hash_g1_g2 and the Miller
+          lines of H_j, W_j once per proposer, then one two-pair Miller loop and ONE final
+          exponentiation per share.
+    `value` is row (b)."""
+    lib = cpu_lib()
     cts = ep["cts"]
     n = len(ep["pk_shares"])
     p = len(cts)
@@ -160,63 +203,134 @@ def cpu_baseline(ep, seconds: float, threads: int):
     off[1:] = np.cumsum([len(c[1]) for c in cts])
     v = np.frombuffer(b"".join(c[1] for c in cts), dtype=np.uint8).copy()
     sh = np.ascontiguousarray(ep["shares"], dtype=np.uint8)
+    threads = all_cores()
 
-    def run(njobs, nthreads, start, fused, nprop=None):
-        k = np.arange(start, start + njobs, dtype=np.uint64)
-        pp = p if nprop is None else nprop
-        jobs = np.stack([(k * 7919) % pp, (k * 104729 + 3) % n], axis=1).astype(np.uint32)
-        out = np.zeros(njobs, dtype=np.uint8)
+    def run(jobs, nthreads, fused):
+        out = np.zeros(len(jobs), dtype=np.uint8)
         t0 = time.perf_counter()
         if fused:
             lib.cpu_verify_dec_shares_fused(pk.ctypes.data, n, u.ctypes.data, v.ctypes.data, off.ctypes.data,
-                                            w.ctypes.data, sh.ctypes.data, p, jobs.ctypes.data, njobs, nthreads,
+                                            w.ctypes.data, sh.ctypes.data, p, jobs.ctypes.data, len(jobs), nthreads,
                                             out.ctypes.data)
         else:
             lib.cpu_verify_dec_shares(pk.ctypes.data, n, u.ctypes.data, v.ctypes.data, off.ctypes.data,
-                                      w.ctypes.data, sh.ctypes.data, jobs.ctypes.data, njobs, nthreads, out.ctypes.data)
+                                      w.ctypes.data, sh.ctypes.data, jobs.ctypes.data, len(jobs), nthreads,
+                                      out.ctypes.data)
         dt = time.perf_counter() - t0
-        expect = ~ep["corrupt"][jobs[:, 0], jobs[:, 1]]
-        assert (out.astype(bool) == expect).all(), "CPU port disagrees with the expected validity"
+        assert (out.astype(bool) == ~ep["corrupt"][jobs[:, 0], jobs[:, 1]]).all(), "CPU port disagrees"
         return dt
 
-    # (a) reference shape
-    t1 = run(2, 1, 0, False) / 2
-    na = max(threads, int(seconds / 2 * threads / t1))
-    da = run(na, threads, 2, False)
-    # (b) hoisted + fused: a sample of whole proposer columns (the per-proposer preparation is part
+    def scattered(count, start):
+        k = np.arange(start, start + count, dtype=np.uint64)
+        return np.stack([(k * 7919) % p, (k * 104729 + 3) % n], axis=1).astype(np.uint32)
+
+    # (a) reference shape, one thread
+    t1 = run(scattered(2, 0), 1, False) / 2
+    na = max(2, int(seconds / 2 / t1))
+    da = run(scattered(na, 2), 1, False)
+    # (b) hoisted + fused, all cores, whole proposer columns (the per-proposer preparation is part
     # of the work and amortises over its n shares, as it does in an epoch)
-    tb1 = run(n, 1, 0, True, nprop=1) / n
-    cols = max(1, min(p, int(seconds / 2 * threads / (tb1 * n))))
-    nb = cols * n
-    kk = np.arange(nb, dtype=np.uint64)
+    col = np.stack([np.zeros(n, np.uint64), np.arange(n, dtype=np.uint64)], axis=1).astype(np.uint32)
+    tb1 = run(col, 1, True) / n
+    cols = max(1, min(p, int(seconds / 2 * min(threads, 64) / (tb1 * n))))
+    kk = np.arange(cols * n, dtype=np.uint64)
     jobs = np.stack([kk // n, kk % n], axis=1).astype(np.uint32)
-    out = np.zeros(nb, dtype=np.uint8)
-    t0 = time.perf_counter()
-    lib.cpu_verify_dec_shares_fused(pk.ctypes.data, n, u.ctypes.data, v.ctypes.data, off.ctypes.data, w.ctypes.data,
-                                    sh.ctypes.data, p, jobs.ctypes.data, nb, threads, out.ctypes.data)
-    db = time.perf_counter() - t0
-    assert (out.astype(bool) == ~ep["corrupt"][jobs[:, 0], jobs[:, 1]]).all(), "fused CPU port disagrees"
+    db = run(jobs, threads, True)
     host = host_info()
-    return dict(value=round(nb / db, 1), unit="share verifies/s", cores=threads, kind="port",
+    return dict(value=round(len(jobs) / db, 1), unit="share verifies/s", cores=threads, kind="port",
                 host=host,
-                rows={"a_reference_shape": {"value": round(na / da, 1), "single_thread": round(1.0 / t1, 2),
-                                            "sample": f"{na} shares in {da:.1f} s"},
-                      "b_hoisted_fused": {"value": round(nb / db, 1), "single_thread": round(1.0 / tb1, 2),
-                                          "sample": f"{cols} proposer columns x {n} shares in {db:.1f} s"}},
-                sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3, {threads} std::threads on {host['model']}, "
-                       f"nproc {host['nproc']}): (b) hash_g1_g2 + lines hoisted per proposer, one 2-pair Miller "
-                       f"loop + one final exponentiation per share, {cols} whole proposer columns of the N={n} "
-                       f"epoch in {db:.1f} s; (a) the reference's per-share shape {na / da:.0f}/s; a restatement, "
-                       f"not the reference binary (no Rust toolchain)")
+                rows={"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
+                                                    "sample": f"{na} shares in {da:.1f} s"},
+                      "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
+                                                    "single_thread": round(1.0 / tb1, 2),
+                                                    "sample": f"{cols} proposer columns x {n} shares in {db:.1f} s"}},
+                sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']} (nproc {host['nproc']}, "
+                       f"affinity {host['affinity']}): (b) {threads} std::threads, hash_g1_g2 + lines hoisted per "
+                       f"proposer, one 2-pair Miller loop + one final exponentiation per share, {cols} whole proposer "
+                       f"columns of the N={n} epoch in {db:.1f} s; (a) 1 thread, the reference's per-share shape, "
+                       f"{na} shares; a restatement, not the reference binary (no Rust toolchain)")
 
 
-def in_flight(args, ep, dev, torch, Context, inputs, pj, maxv, n, t, off, verifies):
+class EpochBench:
+    """One node-epoch (or a proposer slice of one) on device-resident inputs, timed per step."""
+
+    def __init__(self, ctx, ep, dev, stream, torch, verify_lanes, own: bool):
+        self.ctx, self.ep, self.dev, self.stream, self.torch = ctx, ep, dev, stream, torch
+        ctx.set_verify_lanes(verify_lanes)
+        assert (ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]]) == 0).all()
+        if own:
+            ctx.set_own_share(OWN_INDEX, ep["own_sk"])
+        cts = ep["cts"]
+        self.n = len(ep["pk_shares"])
+        self.pj = len(cts)
+        self.t = ep["t"]
+        self.d_u = torch.from_numpy(np.stack([np.frombuffer(c[0], dtype=np.uint8) for c in cts])).to(dev)
+        self.d_w = torch.from_numpy(np.stack([np.frombuffer(c[2], dtype=np.uint8) for c in cts])).to(dev)
+        off = np.zeros(self.pj + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(c[1]) for c in cts])
+        self.off = off
+        self.d_off = torch.from_numpy(off).to(dev)
+        self.d_v = torch.from_numpy(np.frombuffer(b"".join(c[1] for c in cts), dtype=np.uint8).copy()).to(dev)
+        self.d_shares = torch.from_numpy(ep["shares"]).to(dev)
+        self.d_out = torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev)
+        self.maxv = int(np.max(np.diff(off)))
+
+    def bind_outputs(self, d_valid, d_ct_valid, d_status):
+        self.d_valid, self.d_ct_valid, self.d_status = d_valid, d_ct_valid, d_status
+
+    def step(self, events=None):
+        if events:
+            events[0].record(self.stream)
+        # one call per node-epoch (hbx_decrypt_epoch_d): hash_g1_g2 + lines, share checks (the
+        # node's own share check is Ciphertext::verify), combine + decrypt
+        self.ctx.decrypt_epoch_d(self.d_u, self.d_v, self.d_off, self.d_w, self.pj, self.maxv, self.d_shares, self.n,
+                                 self.t, self.d_out, d_valid=self.d_valid, d_ct_valid=self.d_ct_valid,
+                                 d_status=self.d_status, stream=self.stream.cuda_stream)
+        if events:
+            events[1].record(self.stream)
+
+    def check(self, lo):
+        valid = self.d_valid.cpu().numpy().reshape(self.pj, self.n).astype(bool)
+        expect = ~self.ep["corrupt"]
+        assert (self.d_ct_valid.cpu().numpy() == 1).all(), "a valid ciphertext failed Ciphertext::verify"
+        assert (valid == expect).all(), f"validity mismatch at {int((valid != expect).sum())} positions"
+        assert (self.d_status.cpu().numpy() == 0).all(), "combine status"
+        out = self.d_out.cpu().numpy()
+        for j in range(self.pj):
+            assert out[self.off[j]:self.off[j + 1]].tobytes() == self.ep["msgs"][j], f"plaintext {lo + j} differs"
+
+    def kernel_ms(self):
+        kern = {}
+        for name in ("prepare_ct", "prepare_lines", "ct_checks", "verify_shares", "combine"):
+            tot, cnt = self.ctx.kernel_time(name)
+            kern[name] = round(tot / max(cnt, 1), 3)
+        return kern
+
+
+def verify_roofline(shares: int, ms_kernel: float, kernel: str, traffic=None):
+    achieved = shares * VDEC_FQMUL * MADS_PER_FQMUL / (ms_kernel * 1e-3) / 1e12
+    achieved_op = shares * OPCOUNT_VDEC * MADS_PER_FQMUL / (ms_kernel * 1e-3) / 1e12
+    r = {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
+         "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
+         "kernel": kernel, "kernel_ms": ms_kernel,
+         "work": f"{shares} shares x {VDEC_FQMUL} Fq-mul (frozen unit V_dec, SURVEY.md §8(d)) x {MADS_PER_FQMUL} MAD",
+         "opcount": {"fqmul_per_share": OPCOUNT_VDEC, "achieved": round(achieved_op, 3),
+                     "frac": round(achieved_op / PEAK_TMAD_S, 4),
+                     "note": "the current code's own Fq-mul count (tools/opcount), reported beside the frozen unit"}}
+    if traffic:
+        r["traffic"] = traffic["bytes_per_launch"]
+        r["traffic_note"] = (f"PMC FETCH_SIZE+WRITE_SIZE per launch of {traffic['kernel']} at N=256 "
+                             f"({traffic['source']}, commit {traffic.get('commit', '?')}); algorithmic ~1.2e7 B")
+    return r
+
+
+def in_flight(args, eb: EpochBench, dev, torch, Context, verifies):
     """Throughput with `args.in_flight` consecutive epochs overlapping: epoch k on context k mod F
     (own buffers and stream), issued back to back, so one epoch's latency-bound stages (hash-to-G2,
     lines, combine) run beside another's share checks.  The headline `value` stays one epoch at a
     time; this is the node's rate when future-epoch messages are already queued."""
     F = args.in_flight
-    d_u, d_v, d_off, d_w, d_shares = inputs
+    ep, pj, n, off = eb.ep, eb.pj, eb.n, eb.off
     lanes = []
     for _ in range(F):
         c = Context(dev.index or 0)
@@ -232,8 +346,8 @@ def in_flight(args, ep, dev, torch, Context, inputs, pj, maxv, n, t, off, verifi
 
     def issue(k):
         c, st, (o, v, cv, stt) = lanes[k % F]
-        c.decrypt_epoch_d(d_u, d_v, d_off, d_w, pj, maxv, d_shares, n, t, o, d_valid=v, d_ct_valid=cv, d_status=stt,
-                          stream=st.cuda_stream)
+        c.decrypt_epoch_d(eb.d_u, eb.d_v, eb.d_off, eb.d_w, pj, eb.maxv, eb.d_shares, n, eb.t, o, d_valid=v,
+                          d_ct_valid=cv, d_status=stt, stream=st.cuda_stream)
 
     for k in range(F):
         issue(k)
@@ -254,6 +368,353 @@ def in_flight(args, ep, dev, torch, Context, inputs, pj, maxv, n, t, off, verifi
             "value": round(verifies * epochs / elapsed, 1), "unit": "share verifies/s"}
 
 
+def config_c2(args, dev, torch, Context):
+    """BASELINE config 1: N=64, 4,096 decryption-share verifies + 64 combines (t=22) on one GPU."""
+    n = 64
+    stream = torch.cuda.Stream(dev)
+    with Context(dev.index or 0) as ctx:
+        ep = make_epoch(ctx, n, 0, n, args.vlen, args.corrupt_every)
+        eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share)
+        eb.bind_outputs(torch.zeros(n * n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
+                        torch.zeros(n, dtype=torch.int32, device=dev))
+        for _ in range(max(args.warmup, 1)):
+            eb.step()
+        torch.cuda.synchronize(dev)
+        steps = max(args.steps, 5)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+        ctx.set_timing(True)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            eb.step(ev[k])
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        eb.check(0)
+        kern = eb.kernel_ms()
+        ctx.set_timing(False)
+    ms = elapsed / steps * 1e3
+    res = {"workload": f"HoneyBadger node-epoch N={n}: {n * n} decryption-share verifies + {n} Ciphertext::verify + "
+                       f"{n} combines (t={ep['t']}) + decrypt, |v|={args.vlen} B",
+           "value": round(n * n / (elapsed / steps), 1), "unit": "share verifies/s", "ms_per_epoch": round(ms, 3),
+           "epoch_ms_hip_events": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), 3),
+           "kernels_ms": kern,
+           "roofline": verify_roofline(n * n, kern["verify_shares"], "k_verify_shares3 (auto: 64 x 64 checks "
+                                       "fill 1/16 of the chip one lane per check)"),
+           "note": "latency-bound: 4,096 checks leave most SIMDs idle; the per-proposer chains set the time"}
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_dec(ep, args.cpu_seconds)
+    return res
+
+
+# ----------------------------------------------------------------------------------------------
+# Stack B: Common Coin (C4)
+# ----------------------------------------------------------------------------------------------
+def config_c4(args, dev, torch, Context):
+    """BASELINE config 3: CommonCoin for 256 concurrent ABA instances at N=128 (sessions {0,1} x
+    proposers 0..127, agreement epoch 2; nonces as agreement/mod.rs:155-165): 32,768 signature-share
+    verifies (common_coin.rs:151) + 256 combine_signatures + master verifications + parities (:190,
+    :196, :173).  1 in 64 shares replaced by another instance's share of the same signer."""
+    from hbbft_amd import netinfo
+
+    n, inst = 128, 256
+    with Context(dev.index or 0) as ctx:
+        sks, sk_shares, master_sk = netinfo.generate_keys(n)
+        t = sks.threshold + 1
+        pk = ctx.public_keys(sk_shares)
+        master_pk = ctx.public_keys(master_sk)[0].tobytes()
+        assert (ctx.set_pk_shares([r.tobytes() for r in pk]) == 0).all()
+        inv_id = "[" + ", ".join(str(b) for b in master_pk) + "]"
+        nonces = [f"Nonce for Honey Badger {inv_id}@{s}:2:{j}".encode() for s in (0, 1) for j in range(n)]
+        ctx.prepare_nonces(nonces)
+        sigs = ctx.sign(sk_shares)  # (inst, n, 96)
+        rng = np.random.default_rng(0x68626278_00000005)
+        corrupt = rng.integers(0, 64, size=(inst, n)) == 0
+        bad = sigs.copy()
+        ii = np.nonzero(corrupt)
+        bad[ii[0], ii[1]] = sigs[(ii[0] + 1) % inst, ii[1]]
+        steps = max(args.steps, 3)
+        wall = []
+        ctx.prepare_nonces(nonces)  # warm-up round
+        ctx.verify_sig_shares(bad)
+        ctx.combine_signatures(master_pk, t)
+        ctx.set_timing(True)
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            ctx.prepare_nonces(nonces)
+            valid = ctx.verify_sig_shares(bad)
+            sig, st, ok, par = ctx.combine_signatures(master_pk, t)
+            wall.append(time.perf_counter() - t0)
+        kern = {}
+        for name in ("hash_nonces", "prepare_lines", "verify_sig", "combine_sigs"):
+            ms_, cnt_ = ctx.kernel_time(name)
+            kern[name] = round(ms_ / max(cnt_, 1), 3)
+        ctx.set_timing(False)
+    assert (valid == ~corrupt).all(), "signature-share validity"
+    assert (st == 0).all() and ok.all(), "combine / master verification"
+    kms = kern["verify_sig"]
+    achieved = inst * n * VSIG_FQMUL * MADS_PER_FQMUL / (kms * 1e-3) / 1e12
+    achieved_op = inst * n * OPCOUNT_VSIG * MADS_PER_FQMUL / (kms * 1e-3) / 1e12
+    round_kernels = kern["hash_nonces"] + kern["prepare_lines"] + kern["verify_sig"] + kern["combine_sigs"]
+    res = {"workload": f"CommonCoin N={n} x {inst} instances: {inst * n} signature-share verifies + {inst} "
+                       f"combine_signatures (t={t}) + master verifies + parities",
+           "value": round(inst * n / (kms * 1e-3), 1), "unit": "sig-share verifies/s (verify kernel, HIP events)",
+           "round_ms_kernels": round(round_kernels, 3),
+           "round_ms_wall": round(1e3 * float(np.mean(wall)), 3),
+           "wall_note": "host API: the wall time includes PCIe staging of 3.1 MB of signature shares and readbacks",
+           "kernels_ms": kern,
+           "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
+                        "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
+                        "kernel": "k_verify_sig_shares", "kernel_ms": kms,
+                        "work": f"{inst * n} checks x {VSIG_FQMUL} Fq-mul (frozen unit V_sig) x {MADS_PER_FQMUL} MAD",
+                        "opcount": {"fqmul_per_check": OPCOUNT_VSIG, "frac": round(achieved_op / PEAK_TMAD_S, 4)}}}
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_coin(pk, nonces, bad, corrupt, master_pk, t, args.cpu_seconds)
+    return res
+
+
+def cpu_baseline_coin(pk, nonces, sigs, corrupt, master_pk, t, seconds):
+    lib = cpu_lib()
+    inst, n = sigs.shape[:2]
+    pk = np.ascontiguousarray(pk, dtype=np.uint8)
+    blob = np.frombuffer(b"".join(nonces), dtype=np.uint8).copy()
+    off = np.zeros(inst + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(x) for x in nonces])
+    sig = np.ascontiguousarray(sigs, dtype=np.uint8)
+    threads = all_cores()
+
+    def run(jobs, nthreads, fused):
+        out = np.zeros(len(jobs), dtype=np.uint8)
+        t0 = time.perf_counter()
+        lib.cpu_verify_sig_shares(pk.ctypes.data, n, blob.ctypes.data, off.ctypes.data, inst, sig.ctypes.data,
+                                  jobs.ctypes.data, len(jobs), nthreads, fused, out.ctypes.data)
+        dt = time.perf_counter() - t0
+        assert (out.astype(bool) == ~corrupt[jobs[:, 0], jobs[:, 1]]).all(), "CPU coin port disagrees"
+        return dt
+
+    def scattered(count, start):
+        k = np.arange(start, start + count, dtype=np.uint64)
+        return np.stack([(k * 7919) % inst, (k * 104729 + 3) % n], axis=1).astype(np.uint32)
+
+    t1 = run(scattered(2, 0), 1, 0) / 2
+    na = max(2, int(seconds / 2 / t1))
+    da = run(scattered(na, 2), 1, 0)
+    one = np.stack([np.zeros(n, np.uint64), np.arange(n, dtype=np.uint64)], axis=1).astype(np.uint32)
+    tb1 = run(one, 1, 1) / n
+    rows = max(1, min(inst, int(seconds / 2 * min(threads, 64) / (tb1 * n))))
+    kk = np.arange(rows * n, dtype=np.uint64)
+    jobs = np.stack([kk // n, kk % n], axis=1).astype(np.uint32)
+    db = run(jobs, threads, 1)
+    # combine_signatures + master verify + parity of the sampled instances, all cores
+    valid = np.ascontiguousarray(~corrupt, dtype=np.uint8)
+    ok = np.zeros(inst, dtype=np.uint8)
+    par = np.zeros(inst, dtype=np.uint8)
+    mpk = np.frombuffer(master_pk, dtype=np.uint8).copy()
+    t0 = time.perf_counter()
+    lib.cpu_combine_sigs(sig.ctypes.data, valid.ctypes.data, n, rows, t, mpk.ctypes.data, blob.ctypes.data,
+                         off.ctypes.data, threads, ok.ctypes.data, par.ctypes.data)
+    dc = time.perf_counter() - t0
+    assert ok[:rows].all(), "CPU combine / master verification"
+    host = host_info()
+    return dict(value=round(len(jobs) / db, 1), unit="sig-share verifies/s", cores=threads, kind="port", host=host,
+                rows={"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
+                                                    "sample": f"{na} shares in {da:.1f} s"},
+                      "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
+                                                    "single_thread": round(1.0 / tb1, 2),
+                                                    "sample": f"{rows} instances x {n} shares in {db:.1f} s"},
+                      "combine_master_parity_all_cores": {"ms_per_256_instances": round(dc / rows * 256 * 1e3, 1),
+                                                          "sample": f"{rows} instances in {dc:.2f} s"}},
+                sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']}: (a) 1 thread, hash_g2 per "
+                       f"share with pairing 0.14's cofactor multiplication + two pairings; (b) {threads} threads, "
+                       f"H lines per instance + one mixed Miller loop + one final exponentiation per share; a "
+                       f"restatement, not the reference binary")
+
+
+# ----------------------------------------------------------------------------------------------
+# Stack C: Broadcast (C5)
+# ----------------------------------------------------------------------------------------------
+def config_c5(args, dev, torch, Context):
+    """BASELINE config 4: Broadcast at N=128 (f=42), RS(k=44, m=84), 128 instances of a 1 MiB
+    proposal each: encode (broadcast.rs:366) + Merkle roots (:381) + decode with the last 42 shards
+    missing (reconstruct + rebuild + root check + glue, :660-707), for both Merkle digests
+    (SHA-256 as the reference's merkle/ring, and the SHA3 variant north_star names).  Output ==
+    input payload is checked."""
+    from hbbft_amd.hbx import MERKLE_SHA3, MERKLE_SHA256
+
+    n, f = 128, 42
+    k, m = n - 2 * f, 2 * f
+    inst, plen = 128, 1 << 20
+    L = (plen + 4 + k - 1) // k
+    rng = np.random.default_rng(0x68626278_00000006)
+    payload = rng.integers(0, 256, size=(inst, plen), dtype=np.uint8)
+    frame = np.zeros((inst, k * L), dtype=np.uint8)
+    frame[:, :4] = np.frombuffer(np.uint32(plen).byteswap().tobytes(), dtype=np.uint8)
+    frame[:, 4:4 + plen] = payload
+    host = np.zeros((inst, n, L), dtype=np.uint8)
+    host[:, :k] = frame.reshape(inst, k, L)
+    shards = torch.from_numpy(host).to(dev)
+    roots = torch.zeros((inst, 32), dtype=torch.uint8, device=dev)
+    present = torch.ones((inst, n), dtype=torch.uint8, device=dev)
+    present[:, n - f:] = 0
+    out = torch.zeros((inst, k * L), dtype=torch.uint8, device=dev)
+    out_len = torch.zeros(inst, dtype=torch.int64, device=dev)
+    status = torch.zeros(inst, dtype=torch.int32, device=dev)
+    work = torch.empty_like(shards)
+    stream = torch.cuda.Stream(dev)  # events must be recorded on the stream the kernels run on
+    sh = stream.cuda_stream
+    steps = max(args.steps, 3)
+    variants = {}
+    roots_by = {}
+    with Context(dev.index or 0) as ctx, torch.cuda.stream(stream):
+        for name, var in (("sha256", MERKLE_SHA256), ("sha3", MERKLE_SHA3)):
+            ctx.set_merkle_digest(var)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            res = {"encode": [], "roots": [], "decode": [], "step": []}
+            for s in range(steps + 1):
+                if s == 1:
+                    ctx.set_timing(True)  # drop the warm-up step's kernel times
+                ev[0].record(stream)
+                ctx.rs_encode_d(shards, k, m, stream=sh)
+                ev[1].record(stream)
+                ctx.merkle_roots_d(shards, roots, stream=sh)
+                ev[2].record(stream)
+                work.copy_(shards)
+                work[:, n - f:] = 0xA5  # erased shards
+                ev[3].record(stream)
+                ctx.broadcast_decode_d(work, present, roots, k, m, out, out_len, status, stream=sh)
+                ev[4].record(stream)
+                torch.cuda.synchronize(dev)
+                if s:
+                    res["encode"].append(ev[0].elapsed_time(ev[1]))
+                    res["roots"].append(ev[1].elapsed_time(ev[2]))
+                    res["decode"].append(ev[3].elapsed_time(ev[4]))
+                    res["step"].append(ev[0].elapsed_time(ev[2]) + ev[3].elapsed_time(ev[4]))
+            rs_ms, rs_cnt = ctx.kernel_time("rs_code")
+            ml_ms, ml_cnt = ctx.kernel_time("merkle_leaves")
+            ctx.set_timing(False)
+            assert (status.cpu().numpy() == 0).all(), "decode status"
+            assert (out_len.cpu().numpy() == plen).all()
+            assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "decoded payload"
+            roots_by[name] = roots.cpu().numpy().copy()
+            ms = {key: float(np.mean(v)) for key, v in res.items()}
+            leaf_bytes = inst * n * (L + 1)
+            rs_bytes = inst * (k + m) * L  # k L read + m L written per instance
+            ml = ml_ms / max(ml_cnt, 1)
+            variants[name] = {
+                "value": round(inst * plen / (ms["step"] * 1e-3) / 1e9, 2),
+                "unit": "GB/s of proposals (encode + Merkle roots + decode with 42 missing)",
+                "ms": {key: round(v, 3) for key, v in ms.items()},
+                "merkle_leaves_kernel_ms": round(ml, 4),
+                "merkle_leaves_GBps": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),
+                "roofline": {"bound": "hbm", "achieved": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),
+                             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(leaf_bytes / (ml * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                             "traffic": None, "kernel": "k_merkle_leaves" + ("_sha256" if name == "sha256" else "_sha3"),
+                             "work": f"{inst} x {n} leaves of {L + 1} B hashed per launch"},
+            }
+            if name == "sha256":
+                enc = ms["encode"]
+                dwords = inst * (L // 4)
+                enc_valu = dwords * m * k * 4.5  # 3 v_perm_b32 + 1.5 v_bitop3 per (out, in, dword)
+                variants["rs_encode"] = {
+                    "ms": round(enc, 4), "kernel_ms_per_launch": round(rs_ms / max(rs_cnt, 1), 4),
+                    "roofline": {"bound": "valu (v_perm_b32 table lookups)", "achieved": round(rs_bytes / (enc * 1e-3) / 1e9, 1),
+                                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(rs_bytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                 "valu_frac": round(enc_valu / (enc * 1e-3) / PEAK_VALU_OPS, 3),
+                                 "valu_floor_ms": round(enc_valu / PEAK_VALU_OPS * 1e3, 3), "traffic": None,
+                                 "kernel": "k_rs_code_perm",
+                                 "work": f"{inst} x ({k} L read + {m} L written), L = {L}"}}
+    sub = {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} instances of a 1 MiB proposal (shard {L} B)",
+           "value": variants["sha256"]["value"], "unit": variants["sha256"]["unit"],
+           "merkle_sha256": variants["sha256"], "merkle_sha3": variants["sha3"], "rs_encode": variants["rs_encode"]}
+    if not args.no_cpu_baseline:
+        sub["cpu_baseline"] = cpu_baseline_broadcast(host, k, m, L, payload, roots_by, args.cpu_seconds)
+    return sub
+
+
+def _tree_root(leaf_hashes, node):
+    level = list(leaf_hashes)
+    while len(level) > 1:
+        nxt = [node(level[i], level[i + 1]) for i in range(0, len(level) - 1, 2)]
+        if len(level) % 2:
+            nxt.append(level[-1])
+        level = nxt
+    return level[0]
+
+
+def cpu_merkle_root(shards, variant):
+    """merkle (afck) over index-prefixed leaves with OpenSSL's SHA-256 (hashlib; ring uses the same
+    SHA extensions on this CPU), or the SHA3 variant."""
+    n = shards.shape[0]
+    if variant == "sha256":
+        leaf = lambda i: hashlib.sha256(b"\x00" + bytes([i & 0xFF]) + shards[i].tobytes()).digest()  # noqa: E731
+        node = lambda a, b: hashlib.sha256(b"\x01" + a + b).digest()  # noqa: E731
+    else:
+        leaf = lambda i: hashlib.sha3_256(bytes([i & 0xFF]) + shards[i].tobytes()).digest()  # noqa: E731
+        node = lambda a, b: hashlib.sha3_256(a + b).digest()  # noqa: E731
+    return _tree_root([leaf(i) for i in range(n)], node)
+
+
+def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
+    """C5 on host cores: reed-solomon-erasure's table-driven encode / reconstruct
+    (tools/cpu_baseline/cpu_port.cpp) and the Merkle trees with OpenSSL's SHA-256 / SHA3-256
+    (hashlib).  (a) one thread, per instance; (b) all cores over instances (RS: std::threads;
+    Merkle: a thread pool, hashlib releases the GIL on these buffer sizes)."""
+    lib = cpu_lib()
+    inst, n = host_shards.shape[:2]
+    threads = all_cores()
+    # (a) one instance, one thread
+    one = host_shards[:1].copy()
+    t0 = time.perf_counter()
+    lib.cpu_rs_encode(one.ctypes.data, 1, k, m, L, 1)
+    enc1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    r256 = cpu_merkle_root(one[0], "sha256")
+    mk1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    r3 = cpu_merkle_root(one[0], "sha3")
+    mk3 = time.perf_counter() - t0
+    assert r256 == roots_by["sha256"][0].tobytes() and r3 == roots_by["sha3"][0].tobytes(), "CPU Merkle roots"
+    pres = np.ones((1, n), dtype=np.uint8)
+    pres[0, n - (n - k) // 2:] = 0  # the last f missing
+    work = one.copy()
+    work[pres == 0] = 0
+    st = np.zeros(1, dtype=np.int32)
+    t0 = time.perf_counter()
+    lib.cpu_rs_reconstruct(work.ctypes.data, pres.ctypes.data, 1, k, m, L, 1, st.ctypes.data)
+    rec1 = time.perf_counter() - t0
+    dec_root = cpu_merkle_root(work[0], "sha256")
+    assert st[0] == 0 and dec_root == r256 and np.array_equal(work, one), "CPU reconstruct"
+    glued = work[0, :k].reshape(-1)[4:4 + payload.shape[1]]
+    assert np.array_equal(glued, payload[0]), "CPU glue"
+    dec1 = time.perf_counter() - t0
+    # (b) a bounded sample of instances on all cores
+    cnt = max(1, min(inst, int(seconds / 2 * min(threads, 64) / max(enc1 + mk1 + dec1, 1e-3))))
+    many = host_shards[:cnt].copy()
+    t0 = time.perf_counter()
+    lib.cpu_rs_encode(many.ctypes.data, cnt, k, m, L, threads)
+    encb = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as pool:
+        rts = list(pool.map(lambda j: cpu_merkle_root(many[j], "sha256"), range(cnt)))
+    mkb = time.perf_counter() - t0
+    assert all(rts[j] == roots_by["sha256"][j].tobytes() for j in range(cnt)), "CPU Merkle roots (b)"
+    prop = payload.shape[1]
+    host = host_info()
+    gbps = lambda b, s: round(b / s / 1e9, 3)  # noqa: E731
+    return dict(value=gbps(cnt * prop, encb + mkb), unit="GB/s of proposals (encode + SHA-256 Merkle roots)",
+                cores=threads, kind="port", host=host,
+                rows={"a_1thread": {"rs_encode_GBps_hbm_equiv": gbps((k + m) * L, enc1),
+                                    "merkle_sha256_GBps": gbps(n * (L + 1), mk1),
+                                    "merkle_sha3_GBps": gbps(n * (L + 1), mk3),
+                                    "decode_ms_per_instance": round(dec1 * 1e3, 1),
+                                    "ms_per_instance_encode_roots_decode": round((enc1 + mk1 + dec1) * 1e3, 1)},
+                      "b_all_cores": {"rs_encode_GBps_hbm_equiv": gbps(cnt * (k + m) * L, encb),
+                                      "merkle_sha256_GBps": gbps(cnt * n * (L + 1), mkb),
+                                      "sample": f"{cnt} instances on {threads} threads"}},
+                sample=f"RS: tools/cpu_baseline/cpu_port.cpp, reed-solomon-erasure 3.1.0's MUL_TABLE shape "
+                       f"(g++ -O3); Merkle: hashlib (OpenSSL) SHA-256 / SHA3-256; {host['model']}, nproc "
+                       f"{host['nproc']}; a restatement, not the reference binary")
+
+
+# ----------------------------------------------------------------------------------------------
 def main():
     args = parse()
     import torch
@@ -281,50 +742,25 @@ def main():
         lo, hi = 0, n
     pj = hi - lo
     ctx = Context(local)
-    ctx.set_verify_lanes(args.verify_lanes)
     ep = make_epoch(ctx, n, lo, hi, args.vlen, args.corrupt_every)
-    st = ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]])
-    assert (st == 0).all()
-    if not args.no_own_share:
-        ctx.set_own_share(OWN_INDEX, ep["own_sk"])
-
     # a dedicated stream for the epoch calls; the HIP events that time the epoch and the kernels are
     # recorded on the stream the kernels run on
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    sh = stream.cuda_stream
-    assert sh != 0
-    cts = ep["cts"]
-    d_u = torch.from_numpy(np.stack([np.frombuffer(c[0], dtype=np.uint8) for c in cts])).to(dev)
-    d_w = torch.from_numpy(np.stack([np.frombuffer(c[2], dtype=np.uint8) for c in cts])).to(dev)
-    off = np.zeros(pj + 1, dtype=np.int64)
-    off[1:] = np.cumsum([len(c[1]) for c in cts])
-    d_off = torch.from_numpy(off).to(dev)
-    d_v = torch.from_numpy(np.frombuffer(b"".join(c[1] for c in cts), dtype=np.uint8).copy()).to(dev)
-    d_shares = torch.from_numpy(ep["shares"]).to(dev)
-    d_out = torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev)
+    assert stream.cuda_stream != 0
+    eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share)
     # result slab gathered across ranks: [share status pj*n | ct status pj | combine status pj*4],
     # laid out for the largest column block so every rank's slab has the same size
     lay = shard.slab_layout(n, shard.max_columns(n, world) if strong else pj)
     slab = torch.zeros(lay["size"], dtype=torch.uint8, device=dev)
-    d_valid = slab[lay["valid"][0]:lay["valid"][0] + pj * n]
-    d_ct_valid = slab[lay["ct_valid"][0]:lay["ct_valid"][0] + pj]
-    d_status = slab[lay["status"][0]:lay["status"][0] + 4 * pj].view(torch.int32)
+    eb.bind_outputs(slab[lay["valid"][0]:lay["valid"][0] + pj * n], slab[lay["ct_valid"][0]:lay["ct_valid"][0] + pj],
+                    slab[lay["status"][0]:lay["status"][0] + 4 * pj].view(torch.int32))
     gathered = [None]
     t = ep["t"]
-    maxv = int(np.max(np.diff(off)))
-
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
 
     def step(events=None):
-        if events:
-            events[0].record(stream)
-        # one call per node-epoch (hbx_decrypt_epoch_d): hash_g1_g2 + lines, share checks (the
-        # node's own share check is Ciphertext::verify), combine + decrypt
-        ctx.decrypt_epoch_d(d_u, d_v, d_off, d_w, pj, maxv, d_shares, n, t, d_out, d_valid=d_valid,
-                            d_ct_valid=d_ct_valid, d_status=d_status, stream=sh)
-        if events:
-            events[1].record(stream)
+        eb.step(events)
         if strong:
             gathered[0] = shard.all_gather_slabs(slab, world)
 
@@ -349,14 +785,7 @@ def main():
         elapsed = float(tt.item())
 
     # correctness of the last step (size-independent properties)
-    valid = d_valid.cpu().numpy().reshape(pj, n).astype(bool)
-    expect = ~ep["corrupt"]
-    assert (d_ct_valid.cpu().numpy() == 1).all(), "a valid ciphertext failed Ciphertext::verify"
-    assert (valid == expect).all(), f"validity mismatch at {int((valid != expect).sum())} positions"
-    assert (d_status.cpu().numpy() == 0).all(), "combine status"
-    out = d_out.cpu().numpy()
-    for j in range(pj):
-        assert out[off[j]:off[j + 1]].tobytes() == ep["msgs"][j], f"plaintext {lo + j} differs"
+    eb.check(lo)
     if strong:
         gv, gct, gst = shard.assemble(gathered[0].cpu().numpy(), n, world)
         full = np.random.default_rng(0x68626278_00000004).integers(0, args.corrupt_every, size=(n, n)) == 0
@@ -367,15 +796,11 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     verifies = n * n * (1 if strong else world) if args.shard_of <= 1 else pj * n
     value = verifies * args.steps / elapsed
-    shares_here = pj * n
-    kern = {}
-    for name in ("prepare_ct", "prepare_lines", "ct_checks", "verify_shares", "combine"):
-        tot, cnt = ctx.kernel_time(name)
-        kern[name] = round(tot / max(cnt, 1), 3)
+    kern = eb.kernel_ms()
     ctx.set_timing(False)
-    # average launch duration of the dominant kernel, HIP events on its own stream
-    ms_kernel = kern["verify_shares"]
-    achieved = shares_here * FQMUL_PER_SHARE_VERIFY * MADS_PER_FQMUL / (ms_kernel * 1e-3) / 1e12
+    lanes = ctx.verify_lanes_used()
+    kname = {1: "k_verify_shares", 2: "k_verify_shares2", 3: "k_verify_shares3"}.get(lanes, "k_verify_shares")
+    traffic = traffic_record() if (n == 256 and pj == 256) else None
     res = {
         "metric": "BLS12-381 share verifies/sec (node) at N=256; crypto ms per HB epoch",
         "value": round(value, 1),
@@ -398,22 +823,25 @@ def main():
                                    else f"epoch-per-gpu x{world}")},
         "epoch_ms_hip_events": round(float(ms_epoch_ev), 3),
         "kernels_ms": kern,
-        "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
-                     "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4),
-                     "traffic": TRAFFIC_N256_BYTES if (n == 256 and pj == 256) else None,
-                     "traffic_note": "bytes/launch from " + TRAFFIC_SOURCE + " (scratch at Fq12 calls); algorithmic ~1e7",
-                     "kernel": "k_verify_shares", "kernel_ms": ms_kernel,
-                     "work": f"{shares_here} shares x {FQMUL_PER_SHARE_VERIFY} Fq-mul x {MADS_PER_FQMUL} MAD"},
+        "verify_lanes": lanes,
+        "roofline": verify_roofline(pj * n, kern["verify_shares"], kname, traffic),
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
     }
     if world == 1 and args.in_flight > 1:
-        res["epochs_in_flight"] = in_flight(args, ep, dev, torch, Context, (d_u, d_v, d_off, d_w, d_shares), pj, maxv,
-                                            n, t, off, verifies)
+        res["epochs_in_flight"] = in_flight(args, eb, dev, torch, Context, verifies)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(ep, args.cpu_seconds, min(16, os.cpu_count() or 1))
+        res["cpu_baseline"] = cpu_baseline_dec(ep, args.cpu_seconds)
+    ctx.close()
+    if rank == 0 and world == 1 and args.shard_of <= 1 and args.configs:
+        cfgs = {}
+        for name in [c.strip().upper() for c in args.configs.split(",") if c.strip()]:
+            fn = {"C2": config_c2, "C4": config_c4, "C5": config_c5}.get(name)
+            if fn is None:
+                raise SystemExit(f"unknown config {name}")
+            cfgs[name] = fn(args, dev, torch, Context)
+        res["configs"] = cfgs
     if rank == 0:
         print(json.dumps(res), flush=True)
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

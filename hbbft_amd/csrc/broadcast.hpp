@@ -887,7 +887,9 @@ __global__ void __launch_bounds__(256) k_glue(const uint8_t* __restrict__ shards
     return;
   }
   const uint64_t want = ((uint64_t)base[0] << 24) | ((uint64_t)base[1] << 16) | ((uint64_t)base[2] << 8) | base[3];
-  const uint64_t len = want < total - 4 ? want : total - 4;
+  // glue_shards takes at most the bytes there are (broadcast.rs:704); the row holds out_stride
+  uint64_t len = want < total - 4 ? want : total - 4;
+  if (len > out_stride) len = out_stride;
   if (lead) out_len[inst] = len;
   const uint64_t q0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
   if (q0 >= len) return;

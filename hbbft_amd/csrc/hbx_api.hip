@@ -60,7 +60,8 @@ struct hbx_ctx {
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
-  int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1 or 3 lanes per share check
+  int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1, 2 or 3 lanes per share check
+  int lanes_used = 0;                 // lanes per check of the last share-check launch
   // era state
   uint32_t n_keys = 0;
   dbuf pk, pk_m, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk (k_scale_keys)
@@ -80,8 +81,6 @@ struct hbx_ctx {
   // verification state: n_shares / verified_p of the last verify after the latest prepare
   // (0 = none: a prepare invalidates S / valid for the combine)
   uint32_t n_shares = 0, verified_p = 0;
-  const uint8_t* early_shares = nullptr;  // shares decoded by the last prepare (prepare_impl)
-  uint32_t early_n = 0;
   dbuf S, S_status, fallback, valid, shares_own, present_own;
   // combine state
   dbuf keys, status, out_own;
@@ -102,6 +101,13 @@ struct hbx_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> tev[HBX_K_COUNT];
   std::vector<hipEvent_t> ev_pool;
+  // ordering of this context's work across streams: every entry point waits on `ev_last` before
+  // enqueuing on its stream and records it after (stream_scope), so a host call on `stream`
+  // after a _d call on the caller's stream (or on NULL, which does not order against the
+  // non-blocking `stream`) sees that call's results; readouts wait on this event only, not on
+  // the whole device (other contexts' epochs in flight keep running)
+  hipEvent_t ev_last = nullptr;
+  bool ev_recorded = false;
 };
 
 static hipEvent_t ev_get(hbx_ctx* c) {
@@ -158,8 +164,29 @@ static int fail(hbx_ctx* c, int code, const char* fmt, ...) {
   } while (0)
 
 // _d API: the caller's stream; NULL is the HIP null stream (a framework's default stream), so the
-// enqueued work is ordered with the caller's own work on it.
-static hipStream_t pick(hbx_ctx*, void* s) { return static_cast<hipStream_t>(s); }
+// enqueued work is ordered with the caller's own work on it.  The stream first waits for this
+// context's previous work on any stream (ev_last).
+static hipStream_t pick(hbx_ctx* c, void* s) {
+  hipStream_t st = static_cast<hipStream_t>(s);
+  if (c && c->ev_recorded) (void)hipStreamWaitEvent(st, c->ev_last, 0);
+  return st;
+}
+// Records ev_last on the entry point's stream when it returns (on every return path).
+struct stream_scope {
+  hbx_ctx* c;
+  hipStream_t s;
+  ~stream_scope() {
+    if (c && c->ev_last && hipEventRecord(c->ev_last, s) == hipSuccess) c->ev_recorded = true;
+  }
+};
+// Host-side wait for everything this context has enqueued (its own stream and callers' streams).
+static hipError_t quiesce(hbx_ctx* c) {
+  if (c->ev_recorded) {
+    const hipError_t e = hipEventSynchronize(c->ev_last);
+    if (e != hipSuccess) return e;
+  }
+  return hipStreamSynchronize(c->stream);
+}
 
 // bit k = (bytes[k] == 1): status bytes (HBX_SHARE_VALID, HBX_CT_VALID) and 0/1 flags alike
 static void pack_bits(const uint8_t* bytes, size_t n, uint8_t* bits) {
@@ -419,6 +446,11 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
     delete c;
     return HBX_E_DEVICE;
   }
+  if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return HBX_E_DEVICE;
+  }
   *out = c;
   return HBX_OK;
 }
@@ -426,7 +458,7 @@ int hbx_ctx_create(int device, hbx_ctx** out) {
 int hbx_ctx_destroy(hbx_ctx* c) {
   if (!c) return HBX_E_INVALID_ARG;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  (void)quiesce(c);
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
@@ -445,6 +477,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
+  (void)hipEventDestroy(c->ev_last);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return HBX_OK;
@@ -470,6 +503,8 @@ int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
   return HBX_OK;
 }
 
+int hbx_get_verify_lanes_used(const hbx_ctx* c) { return c ? c->lanes_used : 0; }
+
 int hbx_set_merkle_digest(hbx_ctx* c, int variant) {
   if (!c || (variant != HBX_MERKLE_SHA256 && variant != HBX_MERKLE_SHA3))
     return fail(c, HBX_E_INVALID_ARG, "hbx_set_merkle_digest: unknown variant %d", variant);
@@ -483,7 +518,8 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
   // era change: nothing enqueued earlier (on any stream) may still read the old keys, and every
   // state derived from them is void -- the own share (its pk_me check was against the old keys)
   // and the current epoch's prepared ciphertexts / verified shares
-  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, quiesce(c));
+  stream_scope ss_{c, pick(c, c->stream)};
   c->own_me = UINT32_MAX;
   c->own_ready = false;
   c->p_ct = 0;
@@ -535,7 +571,7 @@ int hbx_set_own_share(hbx_ctx* c, uint32_t me, const uint8_t* sk32) {
                ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
   if (!c->own_sk.ensure(32)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_own_share: out of device memory");
   // a prepare enqueued earlier on any stream may still read own_sk
-  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, quiesce(c));
   HIPCHK(c, hipMemcpy(c->own_sk.p, limbs, 32, hipMemcpyHostToDevice));
   c->own_me = me;
   c->own_ready = false;
@@ -551,6 +587,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) || !c->Hj.ensure((size_t)p * sizeof(g2j)) ||
       !c->lines.ensure((size_t)p * sizeof(line_block)) || !c->lines_d.ensure((size_t)p * sizeof(line_block_d)) ||
       !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
@@ -608,8 +645,6 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
   c->ct_known = false;
   c->n_shares = 0;  // S / valid of an earlier verify belong to other ciphertexts
   c->verified_p = 0;
-  c->early_shares = early_shares;
-  c->early_n = early_n;
   if (d_ct_valid) {
     // Ciphertext::verify now: one check per proposer (n = 0 share jobs, job 0 = the ciphertext)
     if (!c->S.ensure(sizeof(g1a)) || !c->S_status.ensure(4) || !c->valid.ensure(16))
@@ -636,6 +671,7 @@ int hbx_prepare_ciphertexts(hbx_ctx* c, const uint8_t* u_comp, const uint8_t* v_
   if (!c || p == 0 || !u_comp || !v_off || !w_comp)
     return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_ciphertexts: bad args");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   const uint64_t vbytes = v_off[p];
   uint64_t maxv = 0;
   for (uint32_t j = 0; j < p; j++) {
@@ -661,22 +697,23 @@ int hbx_prepare_ciphertexts(hbx_ctx* c, const uint8_t* u_comp, const uint8_t* v_
   return HBX_OK;
 }
 
-int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_present, uint32_t n,
-                            uint32_t p, uint8_t* d_valid, void* stream) {
+// Share checks of the prepared ciphertexts.  `predecoded`: the fused epoch call (hbx_decrypt_epoch_d)
+// had prepare_impl decode exactly these shares into S / S_status already.
+static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_present, uint32_t n, uint32_t p,
+                       uint8_t* d_valid, void* stream, bool predecoded) {
   if (!c || !d_shares || n == 0 || p == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_dec_shares_d: bad args");
   if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
   if (p != c->p_ct) return fail(c, HBX_E_NO_CIPHERTEXTS, "p=%u but %u ciphertexts prepared", p, c->p_ct);
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   const size_t m = (size_t)n * p;
   if (!c->S.ensure(m * sizeof(g1a)) || !c->S_status.ensure(m * 4) || !c->valid.ensure(m))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
   // own-share mode: this node's share is the one computed in prepare, and its check IS
   // Ciphertext::verify (k_verify_shares); otherwise the ciphertext checks run separately
   const bool own = c->own_ready && c->own_me < n;
-  if (c->early_shares == d_shares && c->early_n == n) {
-    c->early_shares = nullptr;  // decoded by this epoch's prepare (prepare_impl); used once
-  } else {
+  if (!predecoded) {
     hipLaunchKernelGGL(k_decompress_shares, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, d_shares, m,
                        c->S.as<g1a>(), c->S_status.as<int32_t>(), n, own ? c->own_me : UINT32_MAX,
                        own ? c->own_S.as<g1a>() : nullptr);
@@ -694,6 +731,7 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
     timed t_(c, HBX_K_VERIFY_SHARES, s);
     const size_t waves1 = (size_t)((n + 63) / 64) * p;
     const bool three = c->verify_lanes == 3 || (c->verify_lanes == 0 && waves1 < (size_t)VERIFY_FILL_WAVES);
+    c->lanes_used = three ? 3 : 1;
     if (three)
       hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
                          c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,
@@ -718,10 +756,16 @@ int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* 
   return HBX_OK;
 }
 
+int hbx_verify_dec_shares_d(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_present, uint32_t n,
+                            uint32_t p, uint8_t* d_valid, void* stream) {
+  return verify_impl(c, d_shares, d_present, n, p, d_valid, stream, false);
+}
+
 int hbx_verify_dec_shares(hbx_ctx* c, const uint8_t* shares, const uint8_t* present_bits, uint32_t n,
                           uint32_t p, uint8_t* valid_bits) {
   if (!c || !shares || n == 0 || p == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_dec_shares: bad args");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   const size_t m = (size_t)n * p;
   if (!c->shares_own.ensure(m * 48) || (present_bits && !c->present_own.ensure(m)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares: out of device memory");
@@ -747,6 +791,7 @@ int hbx_rs_encode_d(hbx_ctx* c, uint8_t* d_shards, uint32_t inst, uint32_t k, ui
   if (!c || !d_shards || inst == 0 || L == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_rs_encode_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   if (m == 0) return HBX_OK;  // Coding::Trivial
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
@@ -762,6 +807,7 @@ int hbx_rs_reconstruct_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present
     return fail(c, HBX_E_INVALID_ARG, "hbx_rs_reconstruct_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
   return rs_reconstruct(c, d_shards, d_present, inst, k, m, L, d_status, s);
@@ -771,7 +817,9 @@ int hbx_merkle_roots_d(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint3
                        void* stream) {
   if (!c || !d_shards || !d_roots || inst == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_roots_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
-  return merkle_roots(c, d_shards, inst, n, L, d_roots, pick(c, stream));
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  return merkle_roots(c, d_shards, inst, n, L, d_roots, s);
 }
 
 int hbx_merkle_validate_d(hbx_ctx* c, const uint8_t* d_values, uint32_t vlen, const uint8_t* d_node_hash,
@@ -782,7 +830,9 @@ int hbx_merkle_validate_d(hbx_ctx* c, const uint8_t* d_values, uint32_t vlen, co
       nproofs == 0 || vlen == 0)
     return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_validate_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
-  hipLaunchKernelGGL(k_merkle_validate, dim3((nproofs + 63) / 64), dim3(64), 0, pick(c, stream), d_values, vlen,
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  hipLaunchKernelGGL(k_merkle_validate, dim3((nproofs + 63) / 64), dim3(64), 0, s, d_values, vlen,
                      d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid, c->merkle);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
@@ -795,6 +845,7 @@ int hbx_merkle_build_d(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint3
   if (!c || !d_shards || !d_nodes || inst == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_build_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   uint8_t* roots = d_roots;
   if (!roots) {
     if (!c->roots.ensure((size_t)inst * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "merkle: roots");
@@ -810,7 +861,9 @@ int hbx_merkle_proofs_d(hbx_ctx* c, const uint8_t* d_nodes, uint32_t n, const ui
       n == 0 || n > (uint32_t)RS_MAX_N)
     return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_proofs_d: bad args");
   HIPCHK(c, hipSetDevice(c->device));
-  hipLaunchKernelGGL(k_merkle_proofs, dim3((count + 63) / 64), dim3(64), 0, pick(c, stream), d_nodes, n, d_req, count,
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  hipLaunchKernelGGL(k_merkle_proofs, dim3((count + 63) / 64), dim3(64), 0, s, d_nodes, n, d_req, count,
                      d_node_hash, d_sib_hash, d_sides, d_depth, d_root);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
@@ -821,8 +874,14 @@ int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_prese
                            uint64_t* d_out_len, int32_t* d_status, void* stream) {
   if (!c || !d_shards || !d_present || !d_root_expect || !d_out || !d_out_len || !d_status || inst == 0 || L == 0)
     return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_d: bad args");
+  // the payload length comes from the (untrusted) big-endian header: k L - 4 bytes is the most
+  // glue_shards can take, so every output row must hold that many
+  if ((uint64_t)k * L >= 4 && out_stride < (uint64_t)k * L - 4)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_d: out_stride %llu < k L - 4 = %llu",
+                (unsigned long long)out_stride, (unsigned long long)((uint64_t)k * L - 4));
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
   rc = rs_reconstruct(c, d_shards, d_present, inst, k, m, L, d_status, s);
@@ -849,7 +908,8 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   const uint64_t total = nonce_off[count];
   if (total && !nonce_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_nonces: null blob");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   if (!c->coin_blob.ensure(total ? total : 16) || !c->coin_off.ensure((size_t)(count + 1) * 8) ||
       !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
       !c->coin_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
@@ -890,7 +950,8 @@ int hbx_sign(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* sig96) {
   if (c->coin_I == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "hbx_prepare_nonces has not been called");
   if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_sign: scalar >= r");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   const size_t m = (size_t)n * c->coin_I;
   if (!c->coin_sk.ensure((size_t)n * 32) || !c->coin_sig96.ensure(m * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_sign: out of device memory");
@@ -909,7 +970,8 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
   if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
   if (count != c->coin_I) return fail(c, HBX_E_NO_CIPHERTEXTS, "%u instances but %u nonces prepared", count, c->coin_I);
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   const size_t m = (size_t)n * count;
   if (!c->coin_sig96.ensure(m * 96) || !c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) ||
       !c->coin_valid.ensure(m) || (present_bits && !c->coin_present.ensure(m)))
@@ -949,7 +1011,8 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   const uint64_t total = msg_off[count];
   if (total && !msg_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sigs: null blob");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   if (!c->vs_pk.ensure((size_t)count * 48) || !c->vs_blob.ensure(total ? total : 16) ||
       !c->vs_off.ensure((size_t)(count + 1) * 8) || !c->vs_H.ensure((size_t)count * sizeof(g2a)) ||
       !c->vs_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
@@ -993,7 +1056,8 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
 static int bivar_rows_impl(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32_t t, uint64_t x, bool want48) {
   if (!c || !commit48 || p == 0 || t > 4095) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar: bad args");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   const size_t M = (size_t)(t + 1) * (t + 2) / 2, nr = (size_t)p * (t + 1);
   if (!c->bv_commit48.ensure(p * M * 48) || !c->bv_C.ensure(p * M * sizeof(g1a)) || !c->bv_cst.ensure(p * M * 4) ||
       !c->bv_rows.ensure(nr * sizeof(g1j)) || !c->bv_rows48.ensure(nr * 48) || !c->bv_pst.ensure(p))
@@ -1016,7 +1080,8 @@ int hbx_bivar_rows(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32_t t, 
   if (!rows48 || !status) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar_rows: null output");
   int rc = bivar_rows_impl(c, commit48, p, t, x, true);
   if (rc) return rc;
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   HIPCHK(c, hipMemcpyAsync(rows48, c->bv_rows48.p, (size_t)p * (t + 1) * 48, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipMemcpyAsync(status, c->bv_pst.p, p, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -1032,7 +1097,8 @@ int hbx_bivar_check_acks(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32
     if (ack_proposer[k] >= p) return fail(c, HBX_E_INVALID_ARG, "hbx_bivar_check_acks: proposer %u >= p", ack_proposer[k]);
   int rc = bivar_rows_impl(c, commit48, p, t, x, false);
   if (rc) return rc;
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   if (!c->bv_ackp.ensure((size_t)count * 4) || !c->bv_acky.ensure((size_t)count * 8) ||
       !c->bv_vals.ensure((size_t)count * 32) || !c->bv_out.ensure(count))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_bivar_check_acks: out of device memory");
@@ -1054,7 +1120,8 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
     return fail(c, HBX_E_INVALID_ARG, "hbx_combine_signatures: bad args");
   if (c->coin_n == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified signature shares");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
   const uint32_t I = c->coin_I;
   if (!c->coin_comb.ensure((size_t)I * sizeof(g2a)) || !c->coin_comb_st.ensure((size_t)I * 4) ||
       !c->coin_mpk_comp.ensure(48) || !c->coin_mpk.ensure(sizeof(g1a)) || !c->coin_mpk_st.ensure(4) ||
@@ -1096,7 +1163,9 @@ int hbx_get_ct_valid_d(hbx_ctx* c, uint8_t* d_ct_valid, void* stream) {
   if (!c || !d_ct_valid) return fail(c, HBX_E_INVALID_ARG, "hbx_get_ct_valid_d: bad args");
   if (c->p_ct == 0 || !c->ct_known) return fail(c, HBX_E_NO_CIPHERTEXTS, "ciphertext validity not computed yet");
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, c->p_ct, hipMemcpyDeviceToDevice, pick(c, stream)));
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  HIPCHK(c, hipMemcpyAsync(d_ct_valid, c->ct_valid.p, c->p_ct, hipMemcpyDeviceToDevice, s));
   return HBX_OK;
 }
 
@@ -1107,6 +1176,7 @@ int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* 
     return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified shares for the prepared ciphertexts");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
   const uint32_t p = c->p_ct;
   if (!c->keys.ensure((size_t)p * 32) || !c->status.ensure((size_t)p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_decrypt_d: out of device memory");
@@ -1139,7 +1209,7 @@ int hbx_decrypt_epoch_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
   // occupy every SIMD, and two single-wave-per-SIMD kernels only time-share the VALU.)
   int rc = prepare_impl(c, d_u_comp, d_v_blob, d_v_off, d_w_comp, p, max_v_len, nullptr, stream, d_shares, n);
   if (rc) return rc;
-  rc = hbx_verify_dec_shares_d(c, d_shares, d_present, n, p, d_valid, stream);
+  rc = verify_impl(c, d_shares, d_present, n, p, d_valid, stream, true);
   if (rc) return rc;
   if (d_ct_valid) {
     rc = hbx_get_ct_valid_d(c, d_ct_valid, stream);
@@ -1151,6 +1221,7 @@ int hbx_decrypt_epoch_d(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
 int hbx_combine_decrypt(hbx_ctx* c, uint32_t t, uint8_t* out_blob, int32_t* status) {
   if (!c || !out_blob) return fail(c, HBX_E_INVALID_ARG, "hbx_combine_decrypt: bad args");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   if (c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no ciphertexts prepared");
   std::vector<uint64_t> off(c->p_ct + 1);
   HIPCHK(c, hipMemcpyAsync(off.data(), c->d_v_off, off.size() * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1174,7 +1245,7 @@ static int copy_status(hbx_ctx* c, const dbuf& b, size_t have, uint8_t* out, siz
   if (have == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "%s: nothing computed yet", what);
   if (count != have) return fail(c, HBX_E_INVALID_ARG, "%s: count %zu, expected %zu", what, count, have);
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipDeviceSynchronize());  // the last results may have been enqueued on any stream
+  HIPCHK(c, quiesce(c));  // the last results may have been enqueued on a caller's stream
   HIPCHK(c, hipMemcpy(out, b.p, have, hipMemcpyDeviceToHost));
   return HBX_OK;
 }
@@ -1194,7 +1265,7 @@ int hbx_get_ct_hashes(hbx_ctx* c, uint8_t* h96, size_t count) {
   if (c->p_ct == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "hbx_get_ct_hashes: no ciphertexts prepared");
   if (count != c->p_ct) return fail(c, HBX_E_INVALID_ARG, "hbx_get_ct_hashes: count %zu, expected %u", count, c->p_ct);
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, quiesce(c));
   dbuf out;
   if (!out.ensure(count * 96)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_get_ct_hashes: out of device memory");
   // Hj holds H' = h_eff P = [3(x^2-1)] H (k_prepare_ct); the reference's H = h2 P from it
@@ -1227,6 +1298,7 @@ int hbx_public_keys(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* pk48) 
   if (!c || !sk32 || !pk48 || n == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_public_keys: bad args");
   if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_public_keys: scalar >= r");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   dbuf dsk, dpk;
   if (!dsk.ensure((size_t)n * 32) || !dpk.ensure((size_t)n * 48)) {
     dsk.release();
@@ -1257,6 +1329,7 @@ int hbx_encrypt(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, const 
   const uint64_t total = msg_off[p];
   if (total && (!msg_blob || !v_blob)) return fail(c, HBX_E_INVALID_ARG, "hbx_encrypt: bad args");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   dbuf dpkc, dpk, dst, dr, dm, doff, du, dv, dw;
   dbuf* all[] = {&dpkc, &dpk, &dst, &dr, &dm, &doff, &du, &dv, &dw};
   auto cleanup = [&]() { for (dbuf* b : all) b->release(); };
@@ -1304,6 +1377,7 @@ int hbx_decrypt_shares(hbx_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_
     return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_shares: bad args");
   if (!scalars_canonical(sk32, n)) return fail(c, HBX_E_INVALID_ARG, "hbx_decrypt_shares: scalar >= r");
   HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
   const size_t m = (size_t)n * p;
   dbuf dsk, duc, du, dst, dout;
   dbuf* all[] = {&dsk, &duc, &du, &dst, &dout};

@@ -42,6 +42,7 @@ class EpochResult:
     faults: List[Tuple[int, str]] = field(default_factory=list)  # FaultLog entries, in order
     errors: List[Tuple[int, str]] = field(default_factory=list)  # handle_message -> Err
     batch: Optional[Dict[int, bytes]] = None  # proposer -> contribution, once the epoch output
+    decrypt_errors: List[int] = field(default_factory=list)  # proposers whose decrypt failed (:345)
     ct_status: Dict[int, int] = field(default_factory=dict)  # proposer -> HBX_CT_*
     share_status: List[Optional[int]] = field(default_factory=list)  # per event: HBX_SHARE_* or None
 
@@ -54,11 +55,12 @@ class EpochReplay:
     decryption shares (``decrypt_share_no_verify``, :403) and checks the ciphertexts through
     them."""
 
-    def __init__(self, ctx, n: int, me: int, sk_me: bytes, t: Optional[int] = None):
+    def __init__(self, ctx, n: int, me: int, sk_me: bytes):
         self.ctx = ctx
         self.n = n
         self.f = (n - 1) // 3  # NetworkInfo::num_faulty, messaging.rs:258
-        self.t = self.f + 1 if t is None else t
+        # PublicKeySet::decrypt needs threshold + 1 = f + 1 shares (the key set's threshold is f)
+        self.t = self.f + 1
         self.me = me
         self.sk_me = bytes(sk_me)
 
@@ -170,10 +172,10 @@ class EpochReplay:
                 try_output()
 
         if done:
-            res.batch = self._decrypt(events, props, received, decrypted, len(layers) > 1)
+            res.batch = self._decrypt(events, props, received, decrypted, len(layers) > 1, res.decrypt_errors)
         return res
 
-    def _decrypt(self, events, props, received, decrypted, relayer: bool) -> Dict[int, bytes]:
+    def _decrypt(self, events, props, received, decrypted, relayer: bool, errors: List[int]) -> Dict[int, bytes]:
         """Step 4.  With several messages per pair, verify the final share set once more so the
         engine's combine reads exactly the shares the node ended up holding."""
         p, n = len(props), self.n
@@ -190,7 +192,10 @@ class EpochReplay:
         out = {}
         for j, pid in enumerate(props):
             if pid in decrypted:
-                if st[j] != 0:  # more than f verified shares, yet the engine could not combine
-                    raise RuntimeError(f"combine of proposer {pid} failed with status {st[j]}")
+                if st[j] != 0:
+                    # PublicKeySet::decrypt returned Err: the reference only logs it (:345) and the
+                    # proposer is left out of the batch
+                    errors.append(pid)
+                    continue
                 out[pid] = plains[j]
         return out

@@ -137,6 +137,8 @@ int hbx_set_digest(hbx_ctx* ctx, int variant);
  * per check (~2.5x lower latency per check: epoch shards on one of several GPUs), 0 = choose by
  * launch size (default). */
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
+/* Lanes per check the last decryption-share launch used (1, 2 or 3; 0 before any launch). */
+int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
 int hbx_set_merkle_digest(hbx_ctx* ctx, int variant);
 
 /* ---------------------------------------------------------------------------------------------

@@ -1,6 +1,6 @@
 """Fixtures for the HoneyBadger epoch replay.
 
-    python tests/golden/make_replay.py      # writes tests/golden/hb_replay_{a,b}.npz
+    python tests/golden/make_replay.py      # writes tests/golden/hb_replay_{a,b,c}.npz
 
 One node-epoch of N = 7 nodes as node ``me`` receives it: DecryptionShare messages interleaved
 with the CommonSubset output, including every fault path of honey_badger.rs's decryption sub-path:
@@ -17,7 +17,11 @@ with the CommonSubset output, including every fault path of honey_badger.rs's de
   one (a second message of the same pair)
 * sender 9: not a validator -> Err(UnknownSender)
 * scenario a: messages keep coming after the batch is output (ignored: past epoch);
-  scenario b: proposer 6 never gets more than f shares -> no batch.
+  scenario b: proposer 6 never gets more than f shares -> no batch;
+  scenario c: a Byzantine relayer sends two messages for one (proposer, sender) pair in each
+  order before the ciphertexts are known: sender 3 to proposer 4 a valid then an invalid share
+  (the invalid one replaces it unverified and is removed at the ciphertext: fault, no share),
+  sender 0 to proposer 4 an invalid then a valid share (the valid one replaces it: no fault).
 
 Expected FaultLog / errors / Batch come from the message-at-a-time restatement
 ``oracle/honey_badger.py`` (digest variant SHA-256), plus the expected engine
@@ -121,6 +125,12 @@ def scenario(tag: str):
                 keep += 1
             out.append((i, j, b))
         shares = out
+    if tag == "c":
+        # both pairs' messages go first (before the ciphertexts), in the two orders
+        shares = [s for s in shares if (s[0], s[1]) not in ((3, 4), (0, 4))]
+        bad34 = bls.g1_compress(bls.g1_mul(cts[4][0], sk[3] + 7))
+        bad04 = bls.g1_compress(bls.g1_mul(cts[4][0], sk[0] + 5))
+        shares = [(3, 4, honest(3, 4)), (0, 4, bad04), (3, 4, bad34), (0, 4, honest(0, 4))] + shares
     cut = 4 if tag == "a" else len(shares) // 3  # a: most shares arrive after the ciphertexts
     events = [("share", i, j, b) for (i, j, b) in shares[:cut]]
     events.append(("acs", {j: wire[j] for j in acs_set}))
@@ -213,7 +223,7 @@ def load_events(d):
 
 
 def main():
-    for tag in ("a", "b"):
+    for tag in ("a", "b", "c"):
         d = scenario(tag)
         path = os.path.join(HERE, f"hb_replay_{tag}.npz")
         np.savez_compressed(path, **d)

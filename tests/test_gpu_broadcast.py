@@ -336,3 +336,34 @@ def test_c5_fixture(hbx_ctx, variant):
     torch.cuda.synchronize()
     assert int(st.cpu()[0]) == 0 and int(out_len.cpu()[0]) == plen
     assert hashlib.sha256(out.cpu().numpy()[0, :plen].tobytes()).digest() == g["payload_sha"].tobytes()
+
+
+@pytest.mark.gpu
+def test_broadcast_decode_oversized_header(hbx_ctx):
+    """A Byzantine proposer's length header larger than the payload: glue_shards takes the bytes
+    there are (broadcast.rs:697-707), and an output row shorter than k L - 4 is rejected
+    (the header must never write past the caller's row)."""
+    from hbbft_amd.hbx import HbxError
+
+    n = 7
+    k, m = rm.coding_counts(n)
+    buf = rm.frame_shards(b"payload of a faulty proposer" * 3, n)
+    buf[0, :4] = 0xFF  # BE length 2^32 - 1
+    buf = rm.ReedSolomon(k, m).encode(buf)
+    leaves = [bytes([i]) + buf[i].tobytes() for i in range(n)]
+    tree = rm.MerkleTree(leaves)
+    L = buf.shape[1]
+    want = rm.decode_from_shards(leaves, n, tree.root_hash())
+    assert want is not None and len(want) == k * L - 4
+    present = np.ones((1, n), dtype=np.uint8)
+    root = np.frombuffer(tree.root_hash(), dtype=np.uint8)[None].copy()
+    out = torch.zeros((1, k * L), dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    hbx_ctx.broadcast_decode_d(dev(buf[None]), dev(present), dev(root), k, m, out, out_len, st)
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0 and int(out_len[0]) == k * L - 4
+    assert out[0, : k * L - 4].cpu().numpy().tobytes() == want
+    short = torch.zeros((1, k * L - 5), dtype=torch.uint8, device="cuda")
+    with pytest.raises(HbxError):
+        hbx_ctx.broadcast_decode_d(dev(buf[None]), dev(present), dev(root), k, m, short, out_len, st)

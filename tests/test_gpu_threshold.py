@@ -176,6 +176,37 @@ def test_epochs_in_flight_on_two_contexts():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n64", "hb_epoch_n7"])
+def test_device_calls_then_host_calls(hbx_ctx, name):
+    """_d calls on a caller's stream (not synchronised by the caller), then host calls on the
+    context's own stream (every entry point orders after this context's previous work
+    on any stream).  The host combine and status readouts must see the device calls' results."""
+    import torch
+
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
+    dev = torch.device("cuda", 0)
+    p, n = d["shares"].shape[:2]
+    off = d["v_off"].astype(np.int64)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    t_u, t_w, t_off = up(d["u"]), up(d["w"]), up(off)
+    t_v = up(d["v_blob"].copy() if len(d["v_blob"]) else np.zeros(1, np.uint8))
+    t_sh, t_pr = up(d["shares"]), up(d["present"].astype(np.uint8))
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(dev)
+    hbx_ctx.prepare_ciphertexts_d(t_u, t_v, t_off, t_w, p, int(np.max(np.diff(off))), stream=side.cuda_stream)
+    hbx_ctx.verify_dec_shares_d(t_sh, n, p, d_present=t_pr, stream=side.cuda_stream)
+    # no synchronisation here: the host calls below must order themselves after the side stream
+    plains, status = hbx_ctx.combine_decrypt(int(d["t"]))
+    np.testing.assert_array_equal(hbx_ctx.share_status(p, n), d["expect_share_status"])
+    np.testing.assert_array_equal(hbx_ctx.ct_status(p), d["expect_ct_status"])
+    np.testing.assert_array_equal(status, d["expect_status"])
+    for j, pt in enumerate(plains):
+        if status[j] == 0:
+            _check_plain(d, j, pt)
+
+
+@pytest.mark.gpu
 def test_unknown_sender_status(hbx_ctx):
     """Senders >= n of hbx_set_pk_shares: HBX_SHARE_UNKNOWN_SENDER (the reference returns
     Err(UnknownSender), honey_badger.rs:64-66), never a verification."""

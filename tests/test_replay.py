@@ -91,7 +91,7 @@ class OracleStatusEngine:
         return plains, np.array([0 if x is not None else -3 for x in plains], dtype=np.int32)
 
 
-@pytest.mark.parametrize("tag", ["a", "b"])
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_oracle_restatement_reproduces_fixture(tag):
     from oracle import honey_badger as ohb
     from oracle import threshold as tc
@@ -105,7 +105,7 @@ def test_oracle_restatement_reproduces_fixture(tag):
     assert tc.DEFAULT_DIGEST == "sha256"
 
 
-@pytest.mark.parametrize("tag", ["a", "b"])
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_replay_logic_with_oracle_statuses(tag):
     d = _load(tag)
     events = load_events(d)
@@ -115,7 +115,7 @@ def test_replay_logic_with_oracle_statuses(tag):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["a", "b"])
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_gpu_replay_matches_fixture(hbx_ctx, tag):
     d = _load(tag)
     assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
