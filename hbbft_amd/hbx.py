@@ -196,6 +196,8 @@ class Context:
             raise HbxError(rc, f"hbx_ctx_create(device={device}) failed: no usable HIP device?")
         self.h = h
         self.device = device
+        self._v_off = None  # offsets of the prepared ciphertexts' V blob (host) ...
+        self._d_off = None  # ... or the caller's device tensor of them (device API)
 
     def close(self):
         if getattr(self, "h", None):
@@ -281,6 +283,8 @@ class Context:
     def combine_decrypt(self, t: int):
         """Returns (list of plaintext bytes or None, status int32[p])."""
         off = self._v_off
+        if off is None:  # prepared through the device API: the caller's offsets tensor
+            off = self._d_off.detach().cpu().numpy().astype(np.uint64)
         p = len(off) - 1
         out = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
         st = np.zeros(p, dtype=np.int32)
@@ -368,6 +372,8 @@ class Context:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def prepare_ciphertexts_d(self, d_u, d_v, d_off, d_w, p: int, max_v_len: int, d_ct_valid=None, stream=None):
+        # the host combine_decrypt sizes its output from these offsets (read back when needed)
+        self._v_off, self._d_off = None, d_off
         self._check(self.lib.hbx_prepare_ciphertexts_d(
             self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
             None if d_ct_valid is None else d_ct_valid.data_ptr(), self._stream(stream)))
@@ -516,6 +522,7 @@ class Context:
         """One node-epoch (hbx_decrypt_epoch_d): prepare + share checks (with Ciphertext::verify) +
         combine + decrypt; same results as the three-call sequence."""
         opt = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        self._v_off, self._d_off = None, d_off
         self._check(self.lib.hbx_decrypt_epoch_d(
             self.h, d_u.data_ptr(), d_v.data_ptr(), d_off.data_ptr(), d_w.data_ptr(), p, max_v_len,
             d_shares.data_ptr(), opt(d_present), n, t, opt(d_valid), opt(d_ct_valid), d_out.data_ptr(),
