@@ -590,12 +590,13 @@ HBX_HD void binv_limbs(const uint32_t* x, const uint32_t* m, uint32_t* out) {
 
 // Montgomery inverse: a = x R  ->  binv(a) = x^-1 R^-1, times R^3 in the Montgomery product
 // gives x^-1 R.
-HBX_HDNI fq fq_inv(const fq& a) {
+HBX_HD fq fq_inv_i(const fq& a) {  // inlined copy (no call frame: pairing2d.hpp)
   const fq c = fq_canon(a);
   fq r;
   binv_limbs<12>(c.l, FQ_P, r.l);
   return fq_mul(r, fq_from_const(FQ_R3));
 }
+HBX_HDNI fq fq_inv(const fq& a) { return fq_inv_i(a); }
 
 // Square root for p = 3 mod 4.  Returns false if a is a non-residue.
 HBX_HD bool fq_sqrt(const fq& a, fq& out) {

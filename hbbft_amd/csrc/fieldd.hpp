@@ -44,6 +44,21 @@
 
 namespace hbx {
 
+// A fence between field products whose operands stream from LDS (pairing2d.hpp): the memory
+// clobber makes every later operand read a fresh load (otherwise the compiler keeps an operand
+// loaded for one product live until its reuse several products later), and the scheduling
+// barrier keeps the next product's loads and sums below the current one.  Without it the
+// temporaries of several products are live at once and overflow the register file.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HBX_SEQ()                          \
+  do {                                     \
+    __asm__ volatile("" ::: "memory");     \
+    __builtin_amdgcn_sched_barrier(0);     \
+  } while (0)
+#else
+#define HBX_SEQ() ((void)0)
+#endif
+
 struct fqd {
   int32_t d[14];
 };

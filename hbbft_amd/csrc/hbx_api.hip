@@ -81,7 +81,7 @@ struct hbx_ctx {
   // verification state: n_shares / verified_p of the last verify after the latest prepare
   // (0 = none: a prepare invalidates S / valid for the combine)
   uint32_t n_shares = 0, verified_p = 0;
-  dbuf S, S_status, fallback, valid, shares_own, present_own;
+  dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -465,7 +465,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
-                  &c->S_status, &c->fallback,
+                  &c->S_status, &c->fallback, &c->gslot,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
                   &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef, &c->rs_enc_ptab, &c->rs_ptab_d, &c->rs_ptab_p,
                   &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots,
@@ -497,8 +497,8 @@ int hbx_set_digest(hbx_ctx* c, int variant) {
 }
 
 int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
-  if (!c || (lanes != 0 && lanes != 1 && lanes != 3))
-    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1 or 3, not %d", lanes);
+  if (!c || lanes < 0 || lanes > 3)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1, 2 or 3, not %d", lanes);
   c->verify_lanes = lanes;
   return HBX_OK;
 }
@@ -730,9 +730,20 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
   {
     timed t_(c, HBX_K_VERIFY_SHARES, s);
     const size_t waves1 = (size_t)((n + 63) / 64) * p;
-    const bool three = c->verify_lanes == 3 || (c->verify_lanes == 0 && waves1 < (size_t)VERIFY_FILL_WAVES);
-    c->lanes_used = three ? 3 : 1;
-    if (three)
+    const int lanes = c->verify_lanes ? c->verify_lanes : waves1 < (size_t)VERIFY_FILL_WAVES ? 3 : 2;
+    c->lanes_used = lanes;
+    if (lanes == 2) {
+      // global slots of the final exponentiation: 2 x 78 dwords per lane of the launch
+      const size_t glanes = (size_t)((n + 31) / 32) * p * 64;
+      if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
+        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory (slots)");
+      hipLaunchKernelGGL(k_verify_shares2, dim3((n + 31) / 32, p), dim3(64), 0, s, c->S.as<g1a>(),
+                         c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
+                         c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
+                         own ? c->own_me : UINT32_MAX,
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, c->gslot.as<uint32_t>());
+    }
+    else if (lanes == 3)
       hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
                          c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,
                          c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n,

@@ -18,10 +18,12 @@
 #include "pairing3.hpp"
 #include "pairingd.hpp"
 #include "pairing3d.hpp"
+#include "pairing2d.hpp"
 #include "wide.hpp"
 
 // Split build (tools/build.py): the kernels compile in groups, one translation unit per group
-// (-DHBX_TU=1..6: epoch, share checks, producer, wide checks, coin, broadcast); TU 0 is the host
+// (-DHBX_TU=1..7: epoch, share checks, producer, wide checks, coin, broadcast, two-lane share
+// checks); TU 0 is the host
 // API, which sees only their declarations (_kdecl.hpp, generated from these sources).
 #if !defined(HBX_TU)
 #define HBX_IN_TU(n) 1
@@ -431,6 +433,57 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
     v = check2_g3d(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf, g);
   }
   if (g.gl == 0) {
+    valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+    if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+  }
+}
+#endif
+
+#if HBX_IN_TU(7)
+// k_verify_shares with TWO lanes per share (pairing2d.hpp): lane pair = sender i, blockIdx.y =
+// proposer j, 32 checks per wave.  The throughput kernel of a whole epoch on one GPU: per check the
+// same Fq2-product count as one lane (a little less: scaled lines), half of it on each lane, with
+// the Fq12 state split so that nothing spills; the final exponentiation's saved values sit in two
+// packed LDS slots per lane (FE2_PROG).  Same inputs, outputs and own-share semantics.
+__global__ void __launch_bounds__(64) k_verify_shares2(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
+                                                       const uint8_t* __restrict__ present,
+                                                       const g1a* __restrict__ pk, uint32_t n_keys,
+                                                       const g2a* __restrict__ G2pts,
+                                                       const line_block_d* __restrict__ lines,
+                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
+                                                       uint8_t* __restrict__ valid, uint32_t me,
+                                                       uint8_t* __restrict__ ct_valid, uint32_t* __restrict__ gslot) {
+  // per lane: the Miller loop's scratch, then the final exponentiation's slots A (words 0..77)
+  // and B (78..155); slots G1 (t^3, then d) and G2 (b) in global memory
+  __shared__ uint32_t region[LDS2_DWORDS * 64];
+  const int lane = (int)(threadIdx.x & 63);
+  const bool l1 = (lane & 1) != 0;
+  const uint32_t i = blockIdx.x * 32 + (uint32_t)(lane >> 1);
+  const uint32_t j = blockIdx.y;
+  if (i >= n) return;  // whole pairs
+  const size_t idx = (size_t)j * n + i;
+  const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
+                                     ct_ok[j] != 0);
+  bool v = false;
+  if (res == HBX_SHARE_VALID) {
+    const g1a sh = S[idx], pki = pk[i];
+    const bool skipA = sh.inf || G2pts[2 * j].inf;
+    const bool skipB = pki.inf || G2pts[2 * j + 1].inf;
+    if (skipA && skipB) {
+      v = true;
+    } else {
+      lds_u32* reg = (lds_u32*)region;
+      const int pl = lane & ~1;
+      const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
+      // global slots: [block][slot][word][64 lanes], so a wave's accesses are contiguous
+      uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
+      const slot2<uint32_t*> G1{gb, 64u}, G2{gb + LDS_FQ6D_PACKED * 64, 64u};
+      const uint32_t flags = (l1 ? 1u : 0u) | (skipA ? 0u : 2u) | (skipB ? 0u : 4u);
+      check2d_miller(lines[j].h, sh, lines[j].w, pki, flags, (lds2)(reg + lane), B);
+      v = final_exp2d_is_one(A, B, G1, G2, l1);
+    }
+  }
+  if (!l1) {
     valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
     if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
   }

@@ -12,15 +12,20 @@
 //     product each (the one-lane squaring's two), then c0 = t - ab - v ab, c1 = 2 ab;
 //   * line product: the line c0 + (c1 x) v + y v w is scaled by 1/y (an Fq factor, which the final
 //     exponentiation maps to 1: (p - 1) divides (p^12 - 1)/r), l = (c0/y + (c1 x/y) v) + v w, so
-//     lane k computes A_k (c0' + c1' v) (5 Fq2 products) + v^(2-k) A_(1-k) -- the one-lane sparse
-//     product's 10 Fq2 products and 3 Fq-by-Fq2 products for the y term are 10 products in all;
-//   * general product: lane k computes A_k B_k, and half of the Karatsuba products of
-//     (A0 + A1)(B0 + B1) (three Fq2 products each);
+//     lane k computes A_k (c0' + c1' v) (5 Fq2 products) + v^(2-k) A_(1-k) -- 10 Fq2 products a
+//     line instead of the one-lane sparse product's 10 plus 3 Fq-by-Fq2 products for the y term;
+//   * general product (final exponentiation): lane k computes its own output half as two Fq6
+//     products, X_k Y_0 + [v] X_(1-k) Y_1;
 //   * cyclotomic squaring (Granger-Scott): each lane produces its own three Fq2 coefficients, each
 //     from ONE fused column loop of four digit convolutions and two reductions (lane 0:
 //     a^2 + xi b^2, lane 1: 2 a b; operands selected per lane), the one-lane squaring's 9 Fq2
 //     squarings split evenly;
 //   * Frobenius maps and conjugation are coefficient-wise.
+// Register budget: every Fq6 product streams one operand from LDS (the per-lane region of the
+// block, 156 dwords = one wave per SIMD), one Fq2 coefficient at a time behind a scheduling fence,
+// so a product holds its register operand, three accumulators and one Fq2 product's temporaries
+// (~300 registers: nothing spills).  The Miller loop uses the region unpacked as scratch; the final
+// exponentiation as two packed slots (FE2_PROG).
 // The per-check scalars: lane 0 holds 1/y of both G1 points, lane 1 x/y (one Fq inversion each).
 // Control flow is pair-uniform; every exchange reads the partner lane of the same pair.
 #pragma once
@@ -62,54 +67,181 @@ __device__ __forceinline__ fq6d fq6d_zero() {
   return fq6d{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
 }
 // conj(A0 + A1 w) = A0 - A1 w
-__device__ __forceinline__ fq6d conj2d(const fq6d& a, bool l1) { return l1 ? fq6d_neg(a) : a; }
+// (selects, not a branch: a conditional on an aggregate compiles to divergent control flow with
+// both values live, which made the allocator spill)
+__device__ __forceinline__ fq6d conj2d(const fq6d& a, bool l1) { return sel_t(l1, fq6d_neg(a), a); }
 
-// Miller-loop squaring: (A0 + A1 w)^2 = (t - ab - v ab) + 2 ab w, ab = A0 A1,
-// t = (A0 + A1)(A0 + v A1).  Reduced output.
-__device__ __forceinline__ fq6d sqr2d(const fq6d& A, bool l1) {
-  const fq6d B = xchg_t(A);
-  const fq6d X = sel_t(l1, fq6d_norm(fq6d_add(A, B)), A);
-  const fq6d Y = sel_t(l1, fq6d_norm(fq6d_add(B, fq6d_mul_v(A))), B);
-  const fq6d P = fq6d_mul(X, Y);  // lane 0: ab, lane 1: t
+// ---- the per-lane LDS region: 156 dwords, word k of lane L at k * 64 + L -------------------
+constexpr int LDS2_DWORDS = 156;
+typedef lds_u32* lds2;  // this lane's word 0
+
+__device__ __forceinline__ void lds_put_fq2d_raw(lds2 base, int word, const fq2d& a) {
+  const int32_t* p = reinterpret_cast<const int32_t*>(&a);
+#pragma unroll
+  for (int i = 0; i < 28; i++) base[(word + i) * 64] = (uint32_t)p[i];
+}
+__device__ __forceinline__ fq2d lds_get_fq2d_raw(const lds_u32* base, int word) {
+  fq2d a;
+  int32_t* p = reinterpret_cast<int32_t*>(&a);
+#pragma unroll
+  for (int i = 0; i < 28; i++) p[i] = (int32_t)base[(word + i) * 64];
+  return a;
+}
+// packed: a reduced Fq as 13 dwords (digits 0..12 as 28-bit fields, digit 13 whole), pairingd.hpp
+__device__ __forceinline__ void lds_put_fqd_packed(lds2 base, int word, const fqd& e) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 12; k++) w[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    const uint32_t d = (uint32_t)e.d[i];
+    w[wd] |= d << sh;
+    if (sh > 4) w[wd + 1] |= d >> (32 - sh);
+  }
+  w[12] = (uint32_t)e.d[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) base[(word + k) * 64] = w[k];
+}
+__device__ __forceinline__ fqd lds_get_fqd_packed(const lds_u32* base, int word) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) w[k] = base[(word + k) * 64];
+  fqd e;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    uint32_t d = w[wd] >> sh;
+    if (sh > 4) d |= w[wd + 1] << (32 - sh);
+    e.d[i] = (int32_t)(d & (uint32_t)DMASK);
+  }
+  e.d[13] = (int32_t)w[12];
+  return e;
+}
+constexpr int LDS_FQ6D_PACKED = 78;  // one packed Fq6 half
+__device__ __forceinline__ void lds_put_fq6d_packed(lds2 base, int word, const fq6d& a) {
+  const fqd* e = &a.c0.c0;
+#pragma unroll
+  for (int q = 0; q < 6; q++) lds_put_fqd_packed(base, word + 13 * q, e[q]);
+}
+__device__ __forceinline__ fq2d lds_get_fq2d_packed(const lds_u32* base, int word, int q) {
+  return fq2d{lds_get_fqd_packed(base, word + 26 * q), lds_get_fqd_packed(base, word + 26 * q + 13)};
+}
+__device__ __forceinline__ fq6d lds_get_fq6d_packed(const lds_u32* base, int word) {
+  return fq6d{lds_get_fq2d_packed(base, word, 0), lds_get_fq2d_packed(base, word, 1), lds_get_fq2d_packed(base, word, 2)};
+}
+
+// ---- Fq6 products with the second operand streamed: y(q) returns its Fq2 coefficient q --------
+// Karatsuba (fieldd.hpp fq6d_mul) with each product folded into the output accumulators at once
+// (c0 = t0 + xi (u0 - t1 - t2), c1 = u1 - t0 - t1 + xi t2, c2 = u2 - t0 - t2 + t1); inputs
+// normalised (y's coefficients: sums are formed here); carry-normalised output added to `acc`.
+template <class Y>
+__device__ __forceinline__ void fq6d_mul_acc(fq6d& acc, const fq6d& a, Y y) {
+  {
+    const fq2d t0 = fq2d_mul(a.c0, y(0));
+    acc.c0 = fq2d_add(acc.c0, t0);
+    acc.c1 = fq2d_sub(acc.c1, t0);
+    acc.c2 = fq2d_sub(acc.c2, t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(a.c1, y(1));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
+    acc.c1 = fq2d_sub(acc.c1, t1);
+    acc.c2 = fq2d_add(acc.c2, t1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t2 = fq2d_mul(a.c2, y(2));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
+    acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
+    acc.c2 = fq2d_sub(acc.c2, t2);
+  }
+  HBX_SEQ();
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))));
+  HBX_SEQ();
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))));
+  HBX_SEQ();
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))));
+  HBX_SEQ();
+  acc = fq6d_norm(acc);
+}
+
+// ---- Miller loop -------------------------------------------------------------------------
+// LDS scratch words of the Miller loop: Y of the squaring (unpacked, 84), the scaled line (56)
+constexpr int ML_Y = 0, ML_C0 = 84, ML_C1 = 112;
+
+// (A0 + A1 w)^2 = (t - ab - v ab) + 2 ab w, ab = A0 A1, t = (A0 + A1)(A0 + v A1).  Reduced output.
+__device__ __forceinline__ fq6d sqr2d(const fq6d& A, bool l1, lds2 lds) {
+  fq6d X;
+  {
+    const fq6d B = xchg_t(A);
+    X = sel_t(l1, fq6d_norm(fq6d_add(A, B)), A);
+    const fq6d Y = sel_t(l1, fq6d_norm(fq6d_add(B, fq6d_mul_v(A))), B);
+    lds_put_fq2d_raw(lds, ML_Y, Y.c0);
+    lds_put_fq2d_raw(lds, ML_Y + 28, Y.c1);
+    lds_put_fq2d_raw(lds, ML_Y + 56, Y.c2);
+  }
+  HBX_SEQ();
+  fq6d P = fq6d_zero();  // lane 0: ab, lane 1: t
+  fq6d_mul_acc(P, X, [&](int q) { return lds_get_fq2d_raw(lds, ML_Y + 28 * q); });
   const fq6d Q = xchg_t(P);
   const fq6d r0 = fq6d_sub(fq6d_sub(Q, P), fq6d_mul_v(P));
   const fq6d r1 = fq6d_add(Q, Q);
   return fq6d_reduce(sel_t(l1, r1, r0));
 }
 
-// f * ((c0s + c1s v) + v w): lane 0 A0 L0 + v^2 A1, lane 1 A1 L0 + v A0.  Reduced output.
-__device__ __forceinline__ fq6d line2d(const fq6d& A, const fq2d& c0s, const fq2d& c1s, bool l1) {
-  const fq6d B = xchg_t(A);
-  const fq6d T = fq6d_mul_by_01(A, c0s, c1s);
-  const fq6d vB = fq6d_mul_v(B);
+// f * ((c0s + c1s v) + v w) with the scaled line in LDS: lane 0 A0 L0 + v^2 A1, lane 1
+// A1 L0 + v A0.  A0 L0 by fieldd.hpp fq6d_mul_by_01's Karatsuba (5 Fq2 products).  Reduced output.
+__device__ __forceinline__ fq6d line2d(const fq6d& A, bool l1, lds2 lds) {
+  fq2d c0, c1, c2;
+  {
+    const fq2d t0 = fq2d_mul(A.c0, lds_get_fq2d_raw(lds, ML_C0));
+    c0 = t0;
+    c1 = fq2d_neg(t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(A.c1, lds_get_fq2d_raw(lds, ML_C1));
+    c1 = fq2d_sub(c1, t1);
+    c2 = t1;
+  }
+  HBX_SEQ();
+  c0 = fq2d_add(c0, fq2d_mul_xi(fq2d_mul(A.c2, lds_get_fq2d_raw(lds, ML_C1))));
+  HBX_SEQ();
+  c1 = fq2d_add(c1, fq2d_mul(fq2d_add(A.c0, A.c1), fq2d_add(lds_get_fq2d_raw(lds, ML_C0), lds_get_fq2d_raw(lds, ML_C1))));
+  HBX_SEQ();
+  c2 = fq2d_add(c2, fq2d_mul(A.c2, lds_get_fq2d_raw(lds, ML_C0)));
+  HBX_SEQ();
+  const fq6d T = fq6d_norm(fq6d{c0, c1, c2});
+  const fq6d vB = fq6d_mul_v(xchg_t(A));
   return fq6d_reduce(fq6d_add(T, sel_t(l1, vB, fq6d_mul_v(vB))));
 }
 
-// The scaled line's (c0 / y, c1 x / y): lane 0 holds s = 1/y, lane 1 s = x/y.
-__device__ __forceinline__ void line_eval2d(const line_pre_d& L, const fqd& s, bool l1, fq2d& c0s, fq2d& c1s) {
+// The scaled line's (c0 / y, c1 x / y) into LDS: lane 0 holds s = 1/y, lane 1 s = x/y.
+__device__ __forceinline__ void line_eval2d(const line_pre_d& L, const fqd& s, bool l1, lds2 lds) {
   const fq2d mine = fq2d_mul_fq(sel_t(l1, L.c1, L.c0), s);
   const fq2d other = xchg_t(mine);
-  c0s = sel_t(l1, other, mine);
-  c1s = sel_t(l1, mine, other);
+  lds_put_fq2d_raw(lds, ML_C0, sel_t(l1, other, mine));
+  lds_put_fq2d_raw(lds, ML_C1, sel_t(l1, mine, other));
 }
 
 // Two Miller loops over prepared lines (pairingd.hpp miller_loop2_d), conjugated for x < 0.
-__device__ fq6d miller2d(const line_pre_d* LA, const fqd& sA, bool useA, const line_pre_d* LB, const fqd& sB,
-                         bool useB, bool l1) {
-  fq6d f = l1 ? fq6d_zero() : fq6d_one();
+__device__ __forceinline__ fq6d miller2d(const line_pre_d* LA, const fqd& sA, bool useA, const line_pre_d* LB,
+                                         const fqd& sB, bool useB, bool l1, lds2 lds) {
+  fq6d f = sel_t(l1, fq6d_zero(), fq6d_one());
   int k = 0;
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    if (i != 62) f = sqr2d(f, l1);
+    if (i != 62) f = sqr2d(f, l1, lds);
     const int steps = ((BLS_X >> i) & 1) ? 4 : 2;  // (A, B) lines of the doubling [+ addition]
 #pragma unroll 1
     for (int s = 0; s < steps; s++) {
       const bool b = (s & 1) != 0;
-      const line_pre_d L = ld_uniform((b ? LB : LA) + k);
       if (b ? useB : useA) {
-        fq2d c0s, c1s;
-        line_eval2d(L, b ? sB : sA, l1, c0s, c1s);
-        f = line2d(f, c0s, c1s, l1);
+        line_eval2d(ld_uniform((b ? LB : LA) + k), b ? sB : sA, l1, lds);
+        HBX_SEQ();
+        f = line2d(f, l1, lds);
       }
       if (b) k++;
     }
@@ -117,29 +249,7 @@ __device__ fq6d miller2d(const line_pre_d* LA, const fqd& sA, bool useA, const l
   return conj2d(f, l1);
 }
 
-// General product (A0 + A1 w)(B0 + B1 w) = (A0 B0 + v A1 B1) + ((A0 + A1)(B0 + B1) - A0 B0 - A1 B1) w.
-// Inputs reduced or conjugated reduced; reduced output.
-__device__ __noinline__ fq6d mul2d(const fq6d& X, const fq6d& Y, bool l1) {
-  const fq6d P = fq6d_mul(X, Y);  // lane 0: X0 Y0, lane 1: X1 Y1
-  const fq6d sX = fq6d_norm(fq6d_add(X, xchg_t(X)));
-  const fq6d sY = fq6d_norm(fq6d_add(Y, xchg_t(Y)));
-  // Karatsuba of sX sY: lane 0 the t_i = sX_i sY_i, lane 1 the u_i (pairs of coefficient sums)
-  const fq2d q0 = fq2d_mul(sel_t(l1, fq2d_add(sX.c1, sX.c2), sX.c0), sel_t(l1, fq2d_add(sY.c1, sY.c2), sY.c0));
-  const fq2d q1 = fq2d_mul(sel_t(l1, fq2d_add(sX.c0, sX.c1), sX.c1), sel_t(l1, fq2d_add(sY.c0, sY.c1), sY.c1));
-  const fq2d q2 = fq2d_mul(sel_t(l1, fq2d_add(sX.c0, sX.c2), sX.c2), sel_t(l1, fq2d_add(sY.c0, sY.c2), sY.c2));
-  const fq6d q = fq6d{q0, q1, q2};
-  const fq6d qo = xchg_t(q);
-  const fq6d t = sel_t(l1, qo, q), u = sel_t(l1, q, qo);
-  const fq6d PP = xchg_t(P);
-  if (l1) {
-    const fq2d s0 = fq2d_add(t.c0, fq2d_mul_xi(fq2d_sub(fq2d_sub(u.c0, t.c1), t.c2)));
-    const fq2d s1 = fq2d_add(fq2d_sub(fq2d_sub(u.c1, t.c0), t.c1), fq2d_mul_xi(t.c2));
-    const fq2d s2 = fq2d_add(fq2d_sub(fq2d_sub(u.c2, t.c0), t.c2), t.c1);
-    return fq6d_reduce(fq6d_sub(fq6d_sub(fq6d{s0, s1, s2}, P), PP));
-  }
-  return fq6d_reduce(fq6d_add(P, fq6d_mul_v(PP)));
-}
-
+// ---- final exponentiation --------------------------------------------------------------------
 // Granger-Scott halves: lane 0 a^2 + xi b^2, lane 1 2 a b, as ONE column loop of four digit
 // convolutions re = C1 + C2 - C3, im = C4 + C2 + C3 with
 //   lane 0: C1 = (a0 + a1)(a0 - a1), C2 = (b0 + b1)(b0 - b1), C3 = (2 b0) b1,      C4 = (2 a0) a1;
@@ -190,7 +300,9 @@ __device__ __forceinline__ fq2d cyc_pair2d(const fq2d& a, const fq2d& b, bool l1
 __device__ __forceinline__ fq6d cyc_sqr2d(const fq6d& A, bool l1) {
   const fq6d B = xchg_t(A);
   fq2d T0 = cyc_pair2d(sel_t(l1, A.c2, A.c0), B.c1, l1);
+  HBX_SEQ();
   const fq2d T1 = cyc_pair2d(B.c0, sel_t(l1, A.c1, A.c2), l1);
+  HBX_SEQ();
   const fq2d T2 = cyc_pair2d(sel_t(l1, A.c0, A.c1), B.c2, l1);
   T0 = sel_t(l1, fq2d_mul_xi(T0), T0);
   const fq6d T{T0, T1, T2};
@@ -199,55 +311,324 @@ __device__ __forceinline__ fq6d cyc_sqr2d(const fq6d& A, bool l1) {
   return fq6d_reduce(sel_t(l1, fq6d_add(T3, A2), fq6d_sub(T3, A2)));
 }
 
-// Frobenius maps (fieldd.hpp fq12d_frobenius / fq12d_frobenius2): coefficient q of half k is
-// multiplied by gamma_{1 or 2, 2q + k} (w-basis index; gamma_0 = 1).
-__device__ __forceinline__ fq6d frob2d(const fq6d& A, bool l1) {
-  const fq2d k0 = sel_t(l1, fq2d_const(FROBD1_C1_0, FROBD1_C1_1), fq2d{fqd_const(FQD_ONE), fqd_zero()});
-  const fq2d k1 = sel_t(l1, fq2d_const(FROBD1_C3_0, FROBD1_C3_1), fq2d_const(FROBD1_C2_0, FROBD1_C2_1));
-  const fq2d k2 = sel_t(l1, fq2d_const(FROBD1_C5_0, FROBD1_C5_1), fq2d_const(FROBD1_C4_0, FROBD1_C4_1));
-  return fq6d{fq2d_mul(fq2d_conj(A.c0), k0), fq2d_mul(fq2d_conj(A.c1), k1), fq2d_mul(fq2d_conj(A.c2), k2)};
-}
-__device__ __forceinline__ fq6d frob2_2d(const fq6d& A, bool l1) {
-  const fqd k0 = sel_t(l1, fqd_const(FROBD2_C1), fqd_const(FQD_ONE));
-  const fqd k1 = sel_t(l1, fqd_const(FROBD2_C3), fqd_const(FROBD2_C2));
-  const fqd k2 = sel_t(l1, fqd_const(FROBD2_C5), fqd_const(FROBD2_C4));
-  return fq6d{fq2d_mul_fq(A.c0, k0), fq2d_mul_fq(A.c1, k1), fq2d_mul_fq(A.c2, k2)};
-}
-
-// f^-1 = (A0 - A1 w) / (A0^2 - v A1^2), the Fq6 inverse through field.hpp's 12-limb one.
-__device__ __noinline__ fq6d inv2d(const fq6d& A, bool l1) {
-  const fq6d S = fq6d_mul(A, A);  // lane 0: A0^2, lane 1: A1^2
-  const fq6d So = xchg_t(S);
-  const fq6d N = fq6d_reduce(fq6d_sub(sel_t(l1, So, S), fq6d_mul_v(sel_t(l1, S, So))));
-  const fq6d Ni = fq6d_from_fq6(fq6_inv(fq6d_to_fq6(N)));
-  return fq6d_reduce(conj2d(fq6d_mul(A, Ni), l1));
-}
-
-// g^|x| (g reduced, cyclotomic): squaring runs between the one bits of |x|
-__device__ __noinline__ fq6d cyc_exp_abs_x2d(const fq6d& g, bool l1) {
-  static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
-  fq6d r = g;
-#pragma unroll 1
-  for (int q = 0; q < 6; q++) {
-    const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
-#pragma unroll 1
-    for (int i = 0; i < run; i++) r = cyc_sqr2d(r, l1);
-    if (q < 5) r = mul2d(r, g, l1);
+// ---- Final exponentiation over slots --------------------------------------------------------
+// The working value r lives in LDS slot B between operations, beside slot A (the current
+// exponentiation base or operand); the long-lived t^3 / d sit in a third slot G in global memory
+// (written twice and read twice per check).  Every operation reads its operands from slots and
+// writes its result to a slot, so no large value stays in registers from one operation to the
+// next: each operation is register-allocated on its own (a loop carrying r in registers across
+// its alternative operations spilled the product's operands).  A slot holds this lane's half
+// packed (78 dwords); the pair's halves are at lanes 2m (half 0) and 2m + 1 (half 1).
+// Slot addressing: word k of half h at half_base(h)[k * stride].
+template <class P>
+struct slot2 {
+  P h0;             // half 0 of this pair (the lane-0 column)
+  uint32_t stride;  // dword distance between consecutive words
+  __device__ __forceinline__ P half(int h) const { return h0 + h; }
+};
+template <class P>
+__device__ __forceinline__ fqd slot_get_fqd(P base, uint32_t stride, int word) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) w[k] = base[(word + k) * stride];
+  fqd e;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    uint32_t d = w[wd] >> sh;
+    if (sh > 4) d |= w[wd + 1] << (32 - sh);
+    e.d[i] = (int32_t)(d & (uint32_t)DMASK);
   }
-  return r;
+  e.d[13] = (int32_t)w[12];
+  return e;
+}
+template <class P>
+__device__ __forceinline__ void slot_put_fqd(P base, uint32_t stride, int word, const fqd& e) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 12; k++) w[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    const uint32_t d = (uint32_t)e.d[i];
+    w[wd] |= d << sh;
+    if (sh > 4) w[wd + 1] |= d >> (32 - sh);
+  }
+  w[12] = (uint32_t)e.d[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) base[(word + k) * stride] = w[k];
+}
+template <class P>
+__device__ __forceinline__ fq2d slot_get_fq2d(P base, uint32_t stride, int q) {
+  return fq2d{slot_get_fqd(base, stride, 26 * q), slot_get_fqd(base, stride, 26 * q + 13)};
+}
+template <class P>
+__device__ __forceinline__ void slot_put_fq2d(P base, uint32_t stride, int q, const fq2d& a) {
+  slot_put_fqd(base, stride, 26 * q, a.c0);
+  slot_put_fqd(base, stride, 26 * q + 13, a.c1);
+}
+template <class P>
+__device__ __forceinline__ fq6d slot_get_fq6d(P base, uint32_t stride) {
+  return fq6d{slot_get_fq2d(base, stride, 0), slot_get_fq2d(base, stride, 1), slot_get_fq2d(base, stride, 2)};
+}
+template <class P>
+__device__ __forceinline__ void slot_put_fq6d(P base, uint32_t stride, const fq6d& a) {
+  slot_put_fq2d(base, stride, 0, a.c0);
+  slot_put_fq2d(base, stride, 1, a.c1);
+  slot_put_fq2d(base, stride, 2, a.c2);
 }
 
-// f^(3 (p^12 - 1)/r) (pairingd.hpp final_exponentiation_d, the same chain); g^x = conj(g^|x|)
-__device__ __noinline__ fq6d final_exp2d(const fq6d& f, bool l1) {
-  fq6d t = mul2d(conj2d(f, l1), inv2d(f, l1), l1);
-  t = mul2d(frob2_2d(t, l1), t, l1);
-  fq6d a = mul2d(conj2d(cyc_exp_abs_x2d(t, l1), l1), conj2d(t, l1), l1);  // t^(x-1)
-  a = mul2d(conj2d(cyc_exp_abs_x2d(a, l1), l1), conj2d(a, l1), l1);        // t^((x-1)^2)
-  const fq6d b = mul2d(conj2d(cyc_exp_abs_x2d(a, l1), l1), frob2d(a, l1), l1);  // a^(x+p)
-  fq6d c = mul2d(cyc_exp_abs_x2d(cyc_exp_abs_x2d(b, l1), l1), frob2_2d(b, l1), l1);
-  c = mul2d(c, conj2d(b, l1), l1);                                           // b^(x^2+p^2-1)
-  const fq6d t3 = mul2d(cyc_sqr2d(t, l1), t, l1);                            // t^3
-  return mul2d(c, t3, l1);
+// Fq6 product with BOTH operands streamed (x(q), y(q): Fq2 coefficient q), Karatsuba as
+// fq6d_mul_acc; inputs normalised (or negated normalised); carry-normalised sum added to acc.
+template <class X, class Y>
+__device__ __forceinline__ void fq6d_mul_acc2(fq6d& acc, X x, Y y) {
+  {
+    const fq2d t0 = fq2d_mul(x(0), y(0));
+    acc.c0 = fq2d_add(acc.c0, t0);
+    acc.c1 = fq2d_sub(acc.c1, t0);
+    acc.c2 = fq2d_sub(acc.c2, t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(x(1), y(1));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
+    acc.c1 = fq2d_sub(acc.c1, t1);
+    acc.c2 = fq2d_add(acc.c2, t1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t2 = fq2d_mul(x(2), y(2));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
+    acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
+    acc.c2 = fq2d_sub(acc.c2, t2);
+  }
+  HBX_SEQ();
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(x(1), x(2)), fq2d_add(y(1), y(2)))));
+  HBX_SEQ();
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(x(0), x(1)), fq2d_add(y(0), y(1))));
+  HBX_SEQ();
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(x(0), x(2)), fq2d_add(y(0), y(2))));
+  HBX_SEQ();
+  acc = fq6d_norm(acc);
+}
+
+// B = X * Y with X = slot B (conj first if cx), Y = slot `ys`: lane k's half X_k Y_0 +
+// [v if k = 0] X_(1-k) Y_1; conj of the product if co.  Reads of B all precede the write (one
+// wave, in-order LDS), so the pair's two lanes see the old value.
+template <class P>
+__device__ __forceinline__ void op_mul(const slot2<lds_u32*>& B, const slot2<P>& ys, bool cx, bool co, bool l1) {
+  const lds_u32* xk = B.half(l1 ? 1 : 0);
+  const lds_u32* xo = B.half(l1 ? 0 : 1);
+  fq6d acc = fq6d_zero();
+  // X_k (negated for k = 1 under cx)
+  fq6d_mul_acc2(
+      acc,
+      [&](int q) {
+        const fq2d v = slot_get_fq2d(xk, B.stride, q);
+        return sel_t(cx && l1, fq2d_neg(v), v);
+      },
+      [&](int q) { return slot_get_fq2d(ys.half(0), ys.stride, q); });
+  HBX_SEQ();
+  // W = v X_1 on lane 0 (v (w0, w1, w2) = (xi w2, w0, w1); X_1 negated under cx), X_0 on lane 1
+  fq6d_mul_acc2(
+      acc,
+      [&](int q) {
+        const int qq = l1 ? q : (q + 2) % 3;
+        fq2d v = slot_get_fq2d(xo, B.stride, qq);
+        v = sel_t(cx && !l1, fq2d_neg(v), v);
+        return sel_t(!l1 && q == 0, fq2d_norm(fq2d_mul_xi(v)), v);
+      },
+      [&](int q) { return slot_get_fq2d(ys.half(1), ys.stride, q); });
+  slot_put_fq6d(B.half(l1 ? 1 : 0), B.stride, fq6d_reduce(sel_t(co && l1, fq6d_neg(acc), acc)));
+}
+
+// B = B^(2^n) by cyclotomic squarings in registers
+__device__ __forceinline__ void op_sqr(const slot2<lds_u32*>& B, uint32_t n, bool l1) {
+  lds_u32* mine = B.half(l1 ? 1 : 0);
+  fq6d r = slot_get_fq6d(mine, B.stride);
+#pragma unroll 1
+  for (uint32_t i = 0; i < n; i++) r = cyc_sqr2d(r, l1);
+  slot_put_fq6d(mine, B.stride, r);
+}
+
+// dst = src (own half), or frob / frob2 of it: own coefficient q becomes conj^c(g) K_q with
+// (c, K) = (1, gamma_{1, 2q + k}) for f^p and (0, gamma_{2, 2q + k}) for f^(p^2) (fieldd.hpp
+// fq12d_frobenius / fq12d_frobenius2; gamma_0 = 1; k = this lane's half).  map: 0 copy, 1 frob,
+// 2 frob2.
+template <class PS, class PD>
+__device__ __forceinline__ void op_map(const slot2<PS>& src, const slot2<PD>& dst, int map, bool l1) {
+  const int k = l1 ? 1 : 0;
+  if (map == 0) {
+    const PS s = src.half(k);
+    const PD d = dst.half(k);
+#pragma unroll 6
+    for (int w = 0; w < LDS_FQ6D_PACKED; w++) d[w * dst.stride] = s[w * src.stride];
+    return;
+  }
+#pragma unroll 1
+  for (int q = 0; q < 3; q++) {
+    const int i = 2 * q + k;
+    fq2d c{fqd_const(FQD_ONE), fqd_zero()};
+    if (map == 1) {
+      const int32_t* k0 = i == 1 ? FROBD1_C1_0 : i == 2 ? FROBD1_C2_0 : i == 3 ? FROBD1_C3_0 : i == 4 ? FROBD1_C4_0 : FROBD1_C5_0;
+      const int32_t* k1 = i == 1 ? FROBD1_C1_1 : i == 2 ? FROBD1_C2_1 : i == 3 ? FROBD1_C3_1 : i == 4 ? FROBD1_C4_1 : FROBD1_C5_1;
+      if (i) c = fq2d_const(k0, k1);
+    } else {
+      const int32_t* kk = i == 1 ? FROBD2_C1 : i == 2 ? FROBD2_C2 : i == 3 ? FROBD2_C3 : i == 4 ? FROBD2_C4 : FROBD2_C5;
+      if (i) c = fq2d{fqd_const(kk), fqd_zero()};
+    }
+    fq2d y = slot_get_fq2d(src.half(k), src.stride, q);
+    if (map == 1) y = fq2d_conj(y);
+    slot_put_fq2d(dst.half(k), dst.stride, q, fq2d_mul(y, c));
+  }
+}
+
+// The chain of pairingd.hpp final_exponentiation_d as a program over the slots (regrouped:
+// t^3 is the value after the first step of t^|x|; conj(x^|x|) conj(x) = conj(x^|x| x);
+// d = conj(conj(t^3) b) frob2(b) = t^3 conj(b) frob2(b) before the last two exponentiations).
+// Products always take B * A; the global slots G1 (t^3, then d) and G2 (b) are only copied in and
+// out.  Entry: B = f, A = f^-1.
+enum : uint32_t { FE2_SQR = 0, FE2_MUL = 1, FE2_MAP = 2 };
+enum : uint32_t { FE2_CX = 1, FE2_CO = 2 };  // MUL: conj(X) first, conj of the product
+enum : uint32_t { FE2_S_A = 0, FE2_S_B = 1, FE2_S_G1 = 2, FE2_S_G2 = 3 };  // MAP slots
+#define FE2_MULF(fl) ((uint32_t)FE2_MUL | ((uint32_t)(fl) << 4))
+#define FE2_SQRN(n) ((uint32_t)FE2_SQR | ((uint32_t)(n) << 8))
+#define FE2_MAPOP(m, s, d) ((uint32_t)FE2_MAP | ((uint32_t)(m) << 4) | ((uint32_t)(s) << 8) | ((uint32_t)(d) << 12))
+// B <- B^|x| with the base in A: the runs of squarings between the one bits of |x| (63, 62, 60,
+// 57, 48, 16) and a product by the base after each run but the last
+#define FE2_EXP_TAIL FE2_SQRN(2), FE2_MULF(0), FE2_SQRN(3), FE2_MULF(0), FE2_SQRN(9), FE2_MULF(0), FE2_SQRN(32), \
+    FE2_MULF(0), FE2_SQRN(16)
+#define FE2_EXP FE2_SQRN(1), FE2_MULF(0), FE2_EXP_TAIL
+__constant__ static const uint32_t FE2_PROG[] = {
+    FE2_MULF(FE2_CX),                                            // t0 = conj(f) f^-1
+    FE2_MAPOP(2, FE2_S_B, FE2_S_A), FE2_MULF(0),                 // t = t0 frob2(t0)
+    FE2_MAPOP(0, FE2_S_B, FE2_S_A),                              // A = t
+    FE2_SQRN(1), FE2_MULF(0), FE2_MAPOP(0, FE2_S_B, FE2_S_G1),   // B = t^3 = G1
+    FE2_EXP_TAIL, FE2_MULF(FE2_CO),                              // a = conj(t^|x| t)
+    FE2_MAPOP(0, FE2_S_B, FE2_S_A), FE2_EXP, FE2_MULF(FE2_CO),   // a = conj(a^|x| a)
+    FE2_MAPOP(0, FE2_S_B, FE2_S_A), FE2_EXP,                     // B = a^|x|
+    FE2_MAPOP(1, FE2_S_A, FE2_S_A), FE2_MULF(FE2_CX),            // b = conj(a^|x|) frob(a)
+    FE2_MAPOP(0, FE2_S_B, FE2_S_G2),                             // G2 = b
+    FE2_MAPOP(0, FE2_S_B, FE2_S_A), FE2_MAPOP(0, FE2_S_G1, FE2_S_B),  // A = b, B = t^3
+    FE2_MULF(FE2_CX | FE2_CO),                                   // B = conj(conj(t^3) b)
+    FE2_MAPOP(2, FE2_S_G2, FE2_S_A), FE2_MULF(0),                // B = t^3 conj(b) frob2(b) = d
+    FE2_MAPOP(0, FE2_S_B, FE2_S_G1),                             // G1 = d
+    FE2_MAPOP(0, FE2_S_G2, FE2_S_A), FE2_MAPOP(0, FE2_S_G2, FE2_S_B),  // A = B = b
+    FE2_EXP, FE2_MAPOP(0, FE2_S_B, FE2_S_A), FE2_EXP,            // B = b^(x^2)
+    FE2_MAPOP(0, FE2_S_G1, FE2_S_A), FE2_MULF(0)};               // b^(x^2) d
+#undef FE2_EXP
+#undef FE2_EXP_TAIL
+#undef FE2_MAPOP
+#undef FE2_SQRN
+#undef FE2_MULF
+constexpr int FE2_STEPS = (int)(sizeof(FE2_PROG) / sizeof(FE2_PROG[0]));
+
+// Fq6 inverse in digit form (one Fq inversion, field.hpp's divsteps, inlined: no call frame):
+// c0 = a0^2 - xi a1 a2, c1 = xi a2^2 - a0 a1, c2 = a1^2 - a0 a2, t = a0 c0 + xi (a2 c1 + a1 c2),
+// a^-1 = (c0, c1, c2) / t with t^-1 = conj(t) / (t0^2 + t1^2).  Input reduced; the reduced result
+// goes to `dst` (own half; it also parks (c0, c1, c2) meanwhile).
+__device__ __forceinline__ void fq6d_inv_to(const fq6d& a, lds_u32* dst, uint32_t stride) {
+  fq2d t;
+  {
+    const fq2d c0 = fq2d_reduce(fq2d_sub(fq2d_sqr(a.c0), fq2d_mul_xi(fq2d_mul(a.c1, a.c2))));
+    slot_put_fq2d(dst, stride, 0, c0);
+    t = fq2d_mul(a.c0, c0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d c1 = fq2d_reduce(fq2d_sub(fq2d_mul_xi(fq2d_sqr(a.c2)), fq2d_mul(a.c0, a.c1)));
+    slot_put_fq2d(dst, stride, 1, c1);
+    t = fq2d_add(t, fq2d_mul_xi(fq2d_mul(a.c2, c1)));
+  }
+  HBX_SEQ();
+  {
+    const fq2d c2 = fq2d_reduce(fq2d_sub(fq2d_sqr(a.c1), fq2d_mul(a.c0, a.c2)));
+    slot_put_fq2d(dst, stride, 2, c2);
+    t = fq2d_reduce(fq2d_add(t, fq2d_mul_xi(fq2d_mul(a.c1, c2))));
+  }
+  HBX_SEQ();
+  const fqd nrm = fqd_reduce(fqd_add(fqd_sqr(t.c0), fqd_sqr(t.c1)));
+  HBX_SEQ();
+  const fqd ni = fqd_from_fq(fq_inv_i(fqd_to_fq(nrm)));
+  HBX_SEQ();
+  const fq2d ti = fq2d_mul_fq(fq2d_conj(t), ni);
+#pragma unroll 1
+  for (int q = 0; q < 3; q++) {
+    HBX_SEQ();
+    slot_put_fq2d(dst, stride, q, fq2d_reduce(fq2d_mul(slot_get_fq2d(dst, stride, q), ti)));
+  }
+}
+
+// A = f^-1 = (f0 - f1 w) / (f0^2 - v f1^2) with f in B (own halves).
+__device__ __forceinline__ void op_inv(const slot2<lds_u32*>& A, const slot2<lds_u32*>& B, bool l1) {
+  const lds_u32* fb = B.half(l1 ? 1 : 0);
+  lds_u32* ao = A.half(l1 ? 1 : 0);
+  fq6d S = fq6d_zero();  // lane 0: f0^2, lane 1: f1^2
+  fq6d_mul_acc2(
+      S, [&](int q) { return slot_get_fq2d(fb, B.stride, q); }, [&](int q) { return slot_get_fq2d(fb, B.stride, q); });
+  const fq6d So = xchg_t(S);
+  fq6d_inv_to(fq6d_reduce(fq6d_sub(sel_t(l1, So, S), fq6d_mul_v(sel_t(l1, S, So)))), ao, A.stride);
+  HBX_SEQ();
+  fq6d R = fq6d_zero();
+  fq6d_mul_acc2(
+      R, [&](int q) { return slot_get_fq2d(fb, B.stride, q); }, [&](int q) { return slot_get_fq2d(ao, A.stride, q); });
+  slot_put_fq6d(ao, A.stride, fq6d_reduce(conj2d(R, l1)));
+}
+
+// f^(3 (p^12 - 1)/r) == 1 with f (reduced) in B; A, G1, G2 as above.
+__device__ __forceinline__ bool is_one2d(const fq6d& A, bool l1);
+__device__ __forceinline__ bool final_exp2d_is_one(const slot2<lds_u32*>& A, const slot2<lds_u32*>& B,
+                                                  const slot2<uint32_t*>& G1, const slot2<uint32_t*>& G2, bool l1) {
+  op_inv(A, B, l1);
+#pragma unroll 1
+  for (int pc = 0; pc < FE2_STEPS; pc++) {
+    const uint32_t st = FE2_PROG[pc];
+    const uint32_t op = st & 15;
+    HBX_SEQ();
+    if (op == FE2_SQR) {
+      op_sqr(B, st >> 8, l1);
+    } else if (op == FE2_MUL) {
+      op_mul(B, A, ((st >> 4) & FE2_CX) != 0, ((st >> 4) & FE2_CO) != 0, l1);
+    } else {
+      const int map = (int)((st >> 4) & 15), src = (int)((st >> 8) & 15), dst = (int)((st >> 12) & 15);
+      if (src == FE2_S_B) {
+        if (dst == FE2_S_A) op_map(B, A, map, l1);
+        else if (dst == FE2_S_G1) op_map(B, G1, map, l1);
+        else op_map(B, G2, map, l1);
+      } else if (src == FE2_S_A) {
+        op_map(A, A, map, l1);
+      } else {
+        const slot2<uint32_t*>& g = src == FE2_S_G1 ? G1 : G2;
+        if (dst == FE2_S_A) op_map(g, A, map, l1);
+        else op_map(g, B, map, l1);
+      }
+    }
+  }
+  HBX_SEQ();
+  return is_one2d(slot_get_fq6d(B.half(l1 ? 1 : 0), B.stride), l1);
+}
+
+// The pair's per-check scalars of point P (12-limb affine, not the identity): lane 0 1/y,
+// lane 1 x/y.  `neg`: use -P.
+__device__ __forceinline__ fqd point_scalar2d(const g1a& P, bool neg, bool l1) {
+  const fq y = neg ? fq_neg(P.y) : P.y;
+  const fq yi = fq_inv_i(y);
+  return fqd_from_fq(l1 ? fq_mul(P.x, yi) : yi);
+}
+
+// ---- the whole check ------------------------------------------------------------------------
+// Miller stage: the scalars of both points, the two Miller loops (Miller scratch in the LDS
+// region), f (reduced) to slot B.  flags: bit 0 = this lane is lane 1 of its pair, bit 1 = use
+// pair A (S, H'), bit 2 = use pair B (-[m] pk, W).
+__device__ __forceinline__ void check2d_miller(const line_pre_d* LA, const g1a& PA, const line_pre_d* LB, const g1a& PB,
+                                               uint32_t flags, lds2 lds, const slot2<lds_u32*>& B) {
+  const bool l1 = (flags & 1) != 0, useA = (flags & 2) != 0, useB = (flags & 4) != 0;
+  fqd sA = fqd_zero(), sB = fqd_zero();
+  if (useA) sA = point_scalar2d(PA, false, l1);
+  if (useB) sB = point_scalar2d(PB, true, l1);  // the B point enters negated: -[m] pk_i
+  const fq6d f = miller2d(LA, sA, useA, LB, sB, useB, l1, lds);
+  HBX_SEQ();
+  slot_put_fq6d(B.half(l1 ? 1 : 0), B.stride, fq6d_reduce(f));
 }
 
 // f == 1 for the pair: lane 0 holds (1, 0, 0), lane 1 holds 0
@@ -256,14 +637,6 @@ __device__ __forceinline__ bool is_one2d(const fq6d& A, bool l1) {
   const bool c0ok = l1 ? fq2_is_zero(a.c0) : (fq_eq(a.c0.c0, fq_one()) && fq_is_zero(a.c0.c1));
   const bool mine = c0ok && fq2_is_zero(a.c1) && fq2_is_zero(a.c2);
   return mine && xchg_i32(mine ? 1 : 0) != 0;
-}
-
-// The pair's per-check scalars of point P (12-limb affine, not the identity): lane 0 1/y,
-// lane 1 x/y.  `neg`: use -P.
-__device__ __forceinline__ fqd point_scalar2d(const g1a& P, bool neg, bool l1) {
-  const fq y = neg ? fq_neg(P.y) : P.y;
-  const fq yi = fq_inv(y);
-  return fqd_from_fq(l1 ? fq_mul(P.x, yi) : yi);
 }
 
 #endif  // __HIPCC__

@@ -292,17 +292,20 @@ def test_decrypt_shares_match_oracle(hbx_ctx, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 2])
 @pytest.mark.parametrize("name", ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256",
                                   "hb_epoch_n7_sha3"])
-def test_one_lane_checks_match_golden(hbx_ctx, name):
+def test_one_lane_checks_match_golden(hbx_ctx, name, lanes):
     """The fixtures' launches are small, so the default (auto) path above runs the three-lane
-    share check (pairing3.hpp); this forces the one-lane kernel (hbx_set_verify_lanes(1), what a
-    full N = 256 epoch on one GPU uses) through the same expectations, plain and own-share mode."""
+    share check (pairing3.hpp); this forces the one-lane kernel and the two-lane kernel
+    (pairing2d.hpp: what a full N = 256 epoch on one GPU uses) through the same expectations,
+    plain and own-share mode."""
     d = _load(name)
     _set_keys(hbx_ctx, d)
-    hbx_ctx.set_verify_lanes(1)
+    hbx_ctx.set_verify_lanes(lanes)
     try:
         _device_epoch(hbx_ctx, d, own=False)
+        assert hbx_ctx.verify_lanes_used() == lanes
         hbx_ctx.set_own_share(int(d["own_me"]), d["own_sk"].tobytes())
         try:
             _device_epoch(hbx_ctx, d, own=True)
