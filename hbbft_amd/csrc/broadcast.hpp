@@ -552,12 +552,18 @@ __device__ __forceinline__ void merkle_node(int variant, const uint32_t* l8, con
 
 // Leaf hashes of the index-prefixed shards: leaf(i) = H_leaf([i] || shard_i).
 // grid (ceil(n/64), inst); out: u32[inst][n][8] (digest words, big-endian order).
+// With `slots` (u16[inst][nslots], MERKLE_NO_SLOT = unused) only the listed leaves are hashed,
+// grid (ceil(nslots/64), inst): the decode of validated Echo values hashes only the shards it
+// reconstructed (the others' digests come from the Echo proofs, k_import_leaf_hashes).
+constexpr uint32_t MERKLE_NO_SLOT = 0xFFFFu;
 #if HBX_IN_TU(6)
 __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict__ shards, size_t inst_stride,
                                                       uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
-                                                      int variant) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                      int variant, const uint16_t* __restrict__ slots,
+                                                      uint32_t nslots) {
   const uint32_t inst = blockIdx.y;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slots) i = i < nslots ? slots[(size_t)inst * nslots + i] : MERKLE_NO_SLOT;
   if (i >= n) return;
   uint32_t h[8];
   merkle_leaf_shard(variant, i, shards + (size_t)inst * inst_stride + (size_t)i * L, L, h);
@@ -582,11 +588,16 @@ __device__ __forceinline__ uint32_t sha_sig(uint32_t x, int r1, int r2, int r3) 
 
 #if HBX_IN_TU(6)
 __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __restrict__ shards, size_t inst_stride,
-                                                              uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash) {
+                                                              uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
+                                                              const uint16_t* __restrict__ slots, uint32_t nslots) {
   __shared__ uint4 kw[2][16][64];  // [slot][rounds / 4][lane]
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t i = blockIdx.x * 64 + lane, inst = blockIdx.y;
+  const uint32_t inst = blockIdx.y;
+  uint32_t i = blockIdx.x * 64 + lane;
+  if (slots) i = i < nslots ? slots[(size_t)inst * nslots + i] : MERKLE_NO_SLOT;
   const bool live = i < n;
+  // a block with no leaf to hash (all its slots unused) leaves at once, both waves together
+  if (!__syncthreads_or(live ? 1 : 0)) return;
   const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)(live ? i : 0) * L;
   const uint32_t prefix = (i & 0xFF) << 8;  // bytes 0x00, i
   const uint64_t total = 2 + (uint64_t)L;
@@ -682,6 +693,40 @@ __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __r
 #pragma unroll
     for (int q = 0; q < 8; q++) o[q] = H[q];
   }
+}
+#endif
+
+// Leaf digests handed in by the caller (the Echo proofs' leaf hashes, bytes as on the wire) for
+// every present shard: leaf_hash[inst][i] = BE words of given[inst][i] where present[inst][i].
+#if HBX_IN_TU(6)
+__global__ void k_import_leaf_hashes(const uint8_t* __restrict__ given, const uint8_t* __restrict__ present,
+                                     uint32_t total, uint32_t* __restrict__ leaf_hash) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;  // one digest word
+  if (e >= total * 8 || !present[e / 8]) return;
+  const uint8_t* p = given + (size_t)e * 4;
+  leaf_hash[e] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// The leaves a decode must hash: slots[inst][0..nslots) = the absent shard indices in order, the
+// rest MERKLE_NO_SLOT; none for an instance whose status is already an error (too few shards).
+// One wave per instance (ballot compaction in 64-leaf steps).
+__global__ void __launch_bounds__(64) k_missing_slots(const uint8_t* __restrict__ present, uint32_t n,
+                                                      const int32_t* __restrict__ status, uint32_t nslots,
+                                                      uint16_t* __restrict__ slots) {
+  const uint32_t inst = blockIdx.x, lane = threadIdx.x;
+  uint16_t* out = slots + (size_t)inst * nslots;
+  uint32_t filled = 0;
+  if (status[inst] == 0) {
+    for (uint32_t b = 0; b < n; b += 64) {
+      const uint32_t i = b + lane;
+      const bool miss = i < n && !present[(size_t)inst * n + i];
+      const uint64_t mask = __ballot(miss);
+      const uint32_t pos = filled + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+      if (miss && pos < nslots) out[pos] = (uint16_t)i;
+      filled += (uint32_t)__popcll(mask);
+    }
+  }
+  for (uint32_t q = filled + lane; q < nslots; q += 64) out[q] = (uint16_t)MERKLE_NO_SLOT;
 }
 #endif
 

@@ -87,7 +87,7 @@ struct hbx_ctx {
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
   dbuf gf_log, gf_exp;
   uint32_t rs_k = 0, rs_m = 0;
-  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, roots;
+  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, leaf_slots, roots;
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
@@ -415,10 +415,10 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
     timed t_(c, HBX_K_MERKLE_LEAVES, s);
     if (c->merkle == HBX_MERKLE_SHA256)
       hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((n + 63) / 64, inst), dim3(128), 0, s, d_shards, (size_t)n * L,
-                         n, L, c->leaf_hash.as<uint32_t>());
+                         n, L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u);
     else
       hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                         c->leaf_hash.as<uint32_t>(), c->merkle);
+                         c->leaf_hash.as<uint32_t>(), c->merkle, (const uint16_t*)nullptr, 0u);
   }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots, d_nodes,
@@ -468,7 +468,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->S_status, &c->fallback, &c->gslot,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
                   &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef, &c->rs_enc_ptab, &c->rs_ptab_d, &c->rs_ptab_p,
-                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->roots,
+                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->leaf_slots, &c->roots,
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
@@ -726,11 +726,13 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
     c->ct_known = true;
   }
   // share checks: one lane per check when the launch fills the chip (throughput), else three
-  // lanes per check (latency: an epoch shard on one of several GPUs; pairing3.hpp)
+  // lanes per check (latency: an epoch shard on one of several GPUs; pairing3.hpp).  The two-lane
+  // check (no scratch) measured slower than the one-lane check at N=256 (26.6 vs 24.0 ms,
+  // profiles/r03a_bench.json), so it is only used when asked for.
   {
     timed t_(c, HBX_K_VERIFY_SHARES, s);
     const size_t waves1 = (size_t)((n + 63) / 64) * p;
-    const int lanes = c->verify_lanes ? c->verify_lanes : waves1 < (size_t)VERIFY_FILL_WAVES ? 3 : 2;
+    const int lanes = c->verify_lanes ? c->verify_lanes : waves1 < (size_t)VERIFY_FILL_WAVES ? 3 : 1;
     c->lanes_used = lanes;
     if (lanes == 2) {
       // global slots of the final exponentiation: 2 x 78 dwords per lane of the launch
@@ -880,9 +882,11 @@ int hbx_merkle_proofs_d(hbx_ctx* c, const uint8_t* d_nodes, uint32_t n, const ui
   return HBX_OK;
 }
 
-int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, const uint8_t* d_root_expect,
-                           uint32_t inst, uint32_t k, uint32_t m, uint32_t L, uint8_t* d_out, uint64_t out_stride,
-                           uint64_t* d_out_len, int32_t* d_status, void* stream) {
+// decode_from_shards + glue for `inst` instances; with d_leaf_hash the present shards' leaf digests
+// are taken from it (validated Echo proofs) and only the reconstructed shards are hashed.
+static int broadcast_decode(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, const uint8_t* d_leaf_hash,
+                            const uint8_t* d_root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                            uint8_t* d_out, uint64_t out_stride, uint64_t* d_out_len, int32_t* d_status, void* stream) {
   if (!c || !d_shards || !d_present || !d_root_expect || !d_out || !d_out_len || !d_status || inst == 0 || L == 0)
     return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_d: bad args");
   // the payload length comes from the (untrusted) big-endian header: k L - 4 bytes is the most
@@ -898,8 +902,33 @@ int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_prese
   rc = rs_reconstruct(c, d_shards, d_present, inst, k, m, L, d_status, s);
   if (rc) return rc;
   if (!c->roots.ensure((size_t)inst * 32)) return fail(c, HBX_E_OUT_OF_MEMORY, "decode: roots");
-  rc = merkle_roots(c, d_shards, inst, k + m, L, c->roots.as<uint8_t>(), s);
-  if (rc) return rc;
+  if (d_leaf_hash) {
+    const uint32_t n = k + m;
+    if (n > (uint32_t)RS_MAX_N) return fail(c, HBX_E_INVALID_ARG, "merkle: need 1 <= n <= 256");
+    if (!c->leaf_hash.ensure((size_t)inst * n * 32) || !c->leaf_slots.ensure((size_t)inst * (m ? m : 1) * 2))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "decode: leaf hashes");
+    const uint32_t words = inst * n * 8;
+    hipLaunchKernelGGL(k_import_leaf_hashes, dim3((words + 255) / 256), dim3(256), 0, s, d_leaf_hash, d_present,
+                       inst * n, c->leaf_hash.as<uint32_t>());
+    if (m) {  // Coding::Trivial reconstructs nothing: every shard is present or the status is an error
+      hipLaunchKernelGGL(k_missing_slots, dim3(inst), dim3(64), 0, s, d_present, n, d_status, m,
+                         c->leaf_slots.as<uint16_t>());
+      timed t_(c, HBX_K_MERKLE_LEAVES, s);
+      if (c->merkle == HBX_MERKLE_SHA256)
+        hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((m + 63) / 64, inst), dim3(128), 0, s, d_shards,
+                           (size_t)n * L, n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m);
+      else
+        hipLaunchKernelGGL(k_merkle_leaves, dim3((m + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
+                           c->leaf_hash.as<uint32_t>(), c->merkle, c->leaf_slots.as<uint16_t>(), m);
+    }
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n,
+                       c->roots.as<uint8_t>(), (uint8_t*)nullptr, c->merkle);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    rc = merkle_roots(c, d_shards, inst, k + m, L, c->roots.as<uint8_t>(), s);
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(k_root_check, dim3((inst + 63) / 64), dim3(64), 0, s, c->roots.as<uint8_t>(), d_root_expect, inst,
                      d_status);
   HIPCHK(c, hipGetLastError());
@@ -908,6 +937,22 @@ int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_prese
                      (size_t)out_stride, d_out_len, d_status);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
+}
+
+int hbx_broadcast_decode_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, const uint8_t* d_root_expect,
+                           uint32_t inst, uint32_t k, uint32_t m, uint32_t L, uint8_t* d_out, uint64_t out_stride,
+                           uint64_t* d_out_len, int32_t* d_status, void* stream) {
+  return broadcast_decode(c, d_shards, d_present, nullptr, d_root_expect, inst, k, m, L, d_out, out_stride, d_out_len,
+                          d_status, stream);
+}
+
+int hbx_broadcast_decode_leaves_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_present, const uint8_t* d_leaf_hash,
+                                  const uint8_t* d_root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                                  uint8_t* d_out, uint64_t out_stride, uint64_t* d_out_len, int32_t* d_status,
+                                  void* stream) {
+  if (!d_leaf_hash) return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_leaves_d: d_leaf_hash is NULL");
+  return broadcast_decode(c, d_shards, d_present, d_leaf_hash, d_root_expect, inst, k, m, L, d_out, out_stride,
+                          d_out_len, d_status, stream);
 }
 
 // ---- Common Coin ----------------------------------------------------------------------------

@@ -60,6 +60,7 @@ EXPORTS = (
     "hbx_merkle_roots_d",
     "hbx_merkle_validate_d",
     "hbx_broadcast_decode_d",
+    "hbx_broadcast_decode_leaves_d",
     "hbx_set_timing",
     "hbx_kernel_time",
     "hbx_get_share_status",
@@ -153,6 +154,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_merkle_roots_d.argtypes = [P, P, u32, u32, u32, P, P]
     lib.hbx_merkle_validate_d.argtypes = [P, P, u32, P, P, P, P, P, P, u32, u32, P, P]
     lib.hbx_broadcast_decode_d.argtypes = [P, P, P, P, u32, u32, u32, u32, P, ctypes.c_uint64, P, P, P]
+    lib.hbx_broadcast_decode_leaves_d.argtypes = [P, P, P, P, P, u32, u32, u32, u32, P, ctypes.c_uint64, P, P, P]
     lib.hbx_public_keys.argtypes = [P, u8p, u32, u8p]
     lib.hbx_encrypt.argtypes = [P, u8p, u8p, u64p, u32, u8p, u8p, u8p, u8p]
     lib.hbx_decrypt_shares.argtypes = [P, u8p, u32, u8p, u32, u8p]
@@ -509,6 +511,15 @@ class Context:
         self._check(self.lib.hbx_broadcast_decode_d(
             self.h, d_shards.data_ptr(), d_present.data_ptr(), d_root.data_ptr(), inst, k, m, L, d_out.data_ptr(),
             d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), self._stream(stream)))
+
+    def broadcast_decode_leaves_d(self, d_shards, d_present, d_leaf_hash, d_root, k: int, m: int, d_out, d_out_len,
+                                  d_status, stream=None):
+        """hbx_broadcast_decode_leaves_d: d_leaf_hash uint8[inst, k + m, 32] = the present shards'
+        leaf digests from their validated Echo proofs."""
+        inst, n, L = d_shards.shape
+        self._check(self.lib.hbx_broadcast_decode_leaves_d(
+            self.h, d_shards.data_ptr(), d_present.data_ptr(), d_leaf_hash.data_ptr(), d_root.data_ptr(), inst, k, m,
+            L, d_out.data_ptr(), d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), self._stream(stream)))
 
     def get_ct_valid_d(self, d_ct_valid, stream=None):
         self._check(self.lib.hbx_get_ct_valid_d(self.h, d_ct_valid.data_ptr(), self._stream(stream)))

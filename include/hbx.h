@@ -370,6 +370,16 @@ int hbx_broadcast_decode_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t* d_pre
                            const uint8_t* d_root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
                            uint8_t* d_out, uint64_t out_stride, uint64_t* d_out_len, int32_t* d_status,
                            void* stream);
+/* hbx_broadcast_decode_leaves_d -- the same decode for Echo values that were validated
+ *   (hbx_merkle_validate_d): d_leaf_hash[inst][k + m][32] holds, for every present shard, the leaf
+ *   digest its Echo proof carries (the last lemma node, which validation proved equal to the digest
+ *   of the value).  compute_output rebuilds the tree over those same bytes (broadcast.rs:530-544,
+ *   :683), so only the reconstructed shards are hashed.  Same outputs as
+ *   hbx_broadcast_decode_d when the digests are the values' own. */
+int hbx_broadcast_decode_leaves_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t* d_present,
+                                  const uint8_t* d_leaf_hash, const uint8_t* d_root_expect, uint32_t inst,
+                                  uint32_t k, uint32_t m, uint32_t L, uint8_t* d_out, uint64_t out_stride,
+                                  uint64_t* d_out_len, int32_t* d_status, void* stream);
 
 #ifdef __cplusplus
 }
