@@ -82,12 +82,34 @@ class EpochNode:
         self.batch = None  # proposer -> plaintext, once output
         self.done = False  # the epoch advanced (later messages of it are ignored)
 
-    # -- crypto ---------------------------------------------------------------------------------
+    # -- crypto (one method per threshold_crypto call, so a test can substitute known answers) ----
     def _verify_share(self, sender: int, share, proposer: int, ct) -> bool:
         """HoneyBadger::verify_decryption_share (:222-233)."""
         if sender >= self.n:
             return False
         return tc.verify_decryption_share(self.pk_shares[sender], share, ct, self.variant, hash_pt=self.hashes[proposer])
+
+    def _decode_share(self, share48):
+        return decode_share(share48)
+
+    def _decode_ciphertext(self, ct):
+        return decode_ciphertext(ct)
+
+    def _ciphertext_verify(self, proposer: int, ct) -> bool:
+        """Ciphertext::verify (:371), with hash_g1_g2 kept for the share checks."""
+        h = tc.hash_g1_g2(ct[0], ct[1], self.variant)
+        if not tc.ciphertext_verify(ct, self.variant, hash_pt=h):
+            return False
+        self.hashes[proposer] = h
+        return True
+
+    def _own_share(self, ct):
+        """SecretKeyShare::decrypt_share_no_verify (:403)."""
+        return tc.decrypt_share(self.sk, ct)
+
+    def _decrypt(self, shares, ct) -> bytes:
+        """PublicKeySet::decrypt (:340); raises tc.NotEnoughShares / tc.DuplicateEntry."""
+        return tc.decrypt(self.pk_set, shares, ct, self.variant)
 
     # -- message handlers -------------------------------------------------------------------------
     def handle(self, event):
@@ -98,7 +120,7 @@ class EpochNode:
             if sender >= self.n:
                 self.errors.append((sender, UNKNOWN_SENDER))
                 return
-            dec = decode_share(share48)
+            dec = self._decode_share(share48)
             if dec is None:
                 return  # never reaches HoneyBadger
             self._handle_decryption_share(sender, proposer, dec[1])
@@ -118,15 +140,13 @@ class EpochNode:
     def _send_decryption_shares(self, cs_output):
         cts = {}
         for proposer in sorted(cs_output):
-            ct = decode_ciphertext(cs_output[proposer])
+            ct = self._decode_ciphertext(cs_output[proposer])
             if ct is None:
                 self.faults.append((proposer, INVALID_CIPHERTEXT))
                 continue
-            h = tc.hash_g1_g2(ct[0], ct[1], self.variant)
-            if not tc.ciphertext_verify(ct, self.variant, hash_pt=h):
+            if not self._ciphertext_verify(proposer, ct):
                 self.faults.append((proposer, SHARE_DECRYPTION_FAILED))
                 continue
-            self.hashes[proposer] = h
             # verify_pending_decryption_shares + remove_incorrect_decryption_shares
             pending = self.received.get(proposer, {})
             incorrect = [s for s in sorted(pending) if not self._verify_share(s, pending[s], proposer, ct)]
@@ -134,7 +154,7 @@ class EpochNode:
                 self.faults.append((s, UNVERIFIED_DECRYPTION_SHARE_SENDER))
                 del pending[s]
             # send_decryption_share: our own share, inserted unverified
-            self.received.setdefault(proposer, {})[self.me] = tc.decrypt_share(self.sk, ct)
+            self.received.setdefault(proposer, {})[self.me] = self._own_share(ct)
             cts[proposer] = ct
         self.ciphertexts = cts
         self._try_output_batches()
@@ -150,7 +170,7 @@ class EpochNode:
             return False
         ct = self.ciphertexts[proposer]
         try:
-            self.decrypted[proposer] = tc.decrypt(self.pk_set, sorted(shares.items()), ct, self.variant)
+            self.decrypted[proposer] = self._decrypt(sorted(shares.items()), ct)
         except (tc.NotEnoughShares, tc.DuplicateEntry):
             self.decrypt_errors.append(proposer)
         return True
