@@ -122,6 +122,20 @@ def all_cores() -> int:
     return max(1, os.cpu_count() or 1)
 
 
+def quota_cores():
+    """CPUs the process may actually run on at once: the cgroup v2 cpu.max quota (the GPU box
+    grants a share of the machine), or None when there is no quota below os.cpu_count()."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+        if q == "max":
+            return None
+        c = max(1, int(int(q) / int(period)))
+        return c if c < all_cores() else None
+    except (OSError, ValueError):
+        return None
+
+
 def traffic_record():
     """Newest PMC record for the share check (profiles/*_pmc_hbm.json), or None."""
     import glob
@@ -237,13 +251,19 @@ def cpu_baseline_dec(ep, seconds: float):
     jobs = np.stack([kk // n, kk % n], axis=1).astype(np.uint32)
     db = run(jobs, threads, True)
     host = host_info()
+    rows = {"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
+                                          "sample": f"{na} shares in {da:.1f} s"},
+            "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
+                                          "single_thread": round(1.0 / tb1, 2),
+                                          "sample": f"{cols} proposer columns x {n} shares in {db:.1f} s"}}
+    qc = quota_cores()
+    if qc:  # the same sample on as many threads as the cgroup quota lets run at once
+        dq = run(jobs, qc, True)
+        rows["b_hoisted_fused_quota_cores"] = {"value": round(len(jobs) / dq, 1), "cores": qc,
+                                               "sample": f"same sample in {dq:.1f} s; cgroup cpu.max allows {qc} CPUs"}
     return dict(value=round(len(jobs) / db, 1), unit="share verifies/s", cores=threads, kind="port",
                 host=host,
-                rows={"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
-                                                    "sample": f"{na} shares in {da:.1f} s"},
-                      "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
-                                                    "single_thread": round(1.0 / tb1, 2),
-                                                    "sample": f"{cols} proposer columns x {n} shares in {db:.1f} s"}},
+                rows=rows,
                 sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']} (nproc {host['nproc']}, "
                        f"affinity {host['affinity']}): (b) {threads} std::threads, hash_g1_g2 + lines hoisted per "
                        f"proposer, one 2-pair Miller loop + one final exponentiation per share, {cols} whole proposer "

@@ -537,10 +537,6 @@ __device__ void sha3_node(const uint32_t* l8, const uint32_t* r8, uint32_t* out8
 // Leaves of the broadcast are index-prefixed shards: v = [i as u8] || shard_i (broadcast.rs:373-377).
 constexpr int MERKLE_SHA256 = 0;
 constexpr int MERKLE_SHA3 = 1;
-__device__ __forceinline__ void merkle_leaf_shard(int variant, uint32_t i, const uint8_t* shard, uint64_t L, uint32_t* h) {
-  if (variant == MERKLE_SHA3) sha3_prefixed(i & 0xFF, 1, shard, L, h);
-  else sha256_prefixed((i & 0xFF) << 8, 2, shard, L, h);
-}
 __device__ __forceinline__ void merkle_leaf_value(int variant, const uint8_t* v, uint64_t len, uint32_t* h) {
   if (variant == MERKLE_SHA3) sha3_prefixed(0, 0, v, len, h);
   else sha256_prefixed(0, 1, v, len, h);
@@ -550,28 +546,12 @@ __device__ __forceinline__ void merkle_node(int variant, const uint32_t* l8, con
   else sha256_node(l8, r8, out8);
 }
 
-// Leaf hashes of the index-prefixed shards: leaf(i) = H_leaf([i] || shard_i).
-// grid (ceil(n/64), inst); out: u32[inst][n][8] (digest words, big-endian order).
-// With `slots` (u16[inst][nslots], MERKLE_NO_SLOT = unused) only the listed leaves are hashed,
-// grid (ceil(nslots/64), inst): the decode of validated Echo values hashes only the shards it
-// reconstructed (the others' digests come from the Echo proofs, k_import_leaf_hashes).
+// Leaf hashes of the index-prefixed shards: leaf(i) = H_leaf([i] || shard_i), out u32[inst][n][8]
+// (digest words, big-endian order), by k_merkle_leaves_sha256 / k_merkle_leaves_sha3.  With
+// `slots` (u16[inst][nslots], MERKLE_NO_SLOT = unused) only the listed leaves are hashed: the
+// decode of validated Echo values hashes only the shards it reconstructed (the others' digests
+// come from the Echo proofs, k_import_leaf_hashes).
 constexpr uint32_t MERKLE_NO_SLOT = 0xFFFFu;
-#if HBX_IN_TU(6)
-__global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict__ shards, size_t inst_stride,
-                                                      uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
-                                                      int variant, const uint16_t* __restrict__ slots,
-                                                      uint32_t nslots) {
-  const uint32_t inst = blockIdx.y;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slots) i = i < nslots ? slots[(size_t)inst * nslots + i] : MERKLE_NO_SLOT;
-  if (i >= n) return;
-  uint32_t h[8];
-  merkle_leaf_shard(variant, i, shards + (size_t)inst * inst_stride + (size_t)i * L, L, h);
-  uint32_t* o = leaf_hash + ((size_t)inst * n + i) * 8;
-#pragma unroll
-  for (int q = 0; q < 8; q++) o[q] = h[q];
-}
-#endif
 
 // SHA-256 Merkle leaves (HBX_MERKLE_SHA256), two waves per 64 leaves of one instance:
 //  * wave 1 (producer) loads each leaf's next 64-byte block, expands the message schedule and
@@ -580,7 +560,7 @@ __global__ void __launch_bounds__(64) k_merkle_leaves(const uint8_t* __restrict_
 //  * wave 0 (consumer) runs only the 64 rounds from LDS: the serial chain of a leaf -- the
 //    bound of this kernel, since a C5 epoch has just n x inst = 16,384 independent leaves of 373
 //    blocks each -- carries no global loads, no schedule and no scratch round trips.
-// Same digests as k_merkle_leaves (leaf = SHA-256(0x00 || i || shard_i)).
+// leaf = SHA-256(0x00 || i || shard_i) (merkle.rs with ring).
 // grid (ceil(n / 64), inst), 128 threads.
 __device__ __forceinline__ uint32_t sha_sig(uint32_t x, int r1, int r2, int r3) {
   return xor3(rotr32(x, r1), rotr32(x, r2), rotr32(x, r3));
@@ -727,6 +707,170 @@ __global__ void __launch_bounds__(64) k_missing_slots(const uint8_t* __restrict_
     }
   }
   for (uint32_t q = filled + lane; q < nslots; q += 64) out[q] = (uint16_t)MERKLE_NO_SLOT;
+}
+#endif
+
+// SHA3 Merkle leaves (HBX_MERKLE_SHA3), TWO lanes per leaf, bit-interleaved Keccak-f[1600]: the
+// lane pair (2m, 2m + 1) holds the even bits (lane 2m) and the odd bits (lane 2m + 1) of all 25
+// state words as 32-bit halves (the classic 32-bit technique).  A 64-bit rotation by 2k is a 32-bit
+// rotation by k of both halves; by 2k + 1 it swaps the halves between the lanes (one DPP quad
+// permutation) with rotations by k + 1 (even) and k (odd).  pi, chi and iota are half-local, so a
+// round costs a lane ~115 VALU ops against ~190 for a whole-word round, and a C5 epoch's 16,384
+// leaves fill 512 waves instead of 256 (the one-lane kernel left three SIMDs of four idle).
+// leaf = SHA3-256([i] || shard_i), as sha3_prefixed computes it on one lane (k_merkle_validate).
+// grid (ceil(n / 32), inst) [or ceil(nslots / 32) with slots], 64 threads.
+#if HBX_IN_TU(6)
+__device__ __forceinline__ uint32_t k_xchg(uint32_t v) {  // quad_perm [1, 0, 3, 2]: the pair partner
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t rotl32c(uint32_t x, uint32_t k) { return __builtin_amdgcn_alignbit(x, x, (32u - k) & 31u); }
+__device__ __forceinline__ uint32_t even16(uint32_t x) {  // bits 0, 2, .., 30 -> bits 0..15
+  x &= 0x55555555u;
+  x = (x | (x >> 1)) & 0x33333333u;
+  x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+  x = (x | (x >> 4)) & 0x00FF00FFu;
+  return (x | (x >> 8)) & 0x0000FFFFu;
+}
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {  // bits 0..15 -> bits 0, 2, .., 30
+  x &= 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  return (x | (x << 1)) & 0x55555555u;
+}
+// this lane's half of the 64-bit word (lo, hi): h = 0 the even bits, h = 1 the odd bits
+__device__ __forceinline__ uint32_t ileave_half(uint32_t lo, uint32_t hi, uint32_t h) {
+  return even16(lo >> h) | (even16(hi >> h) << 16);
+}
+constexpr uint32_t rc_half(uint64_t rc, int h) {
+  uint32_t r = 0;
+  for (int b = 0; b < 32; b++) r |= (uint32_t)((rc >> (2 * b + h)) & 1u) << b;
+  return r;
+}
+struct keccak_rc_halves {
+  uint32_t e[24], o[24];
+  constexpr keccak_rc_halves() : e(), o() {
+    constexpr uint64_t RC[24] = {
+        0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+        0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+        0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+        0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+        0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+        0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+    for (int r = 0; r < 24; r++) {
+      e[r] = rc_half(RC[r], 0);
+      o[r] = rc_half(RC[r], 1);
+    }
+  }
+};
+// Keccak-f[1600] on this lane's halves a[5 y + x]
+__device__ __forceinline__ void keccak_f1600_il(uint32_t* a, uint32_t h) {
+  constexpr keccak_rc_halves RCH{};
+  constexpr int RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+#pragma unroll
+  for (int r = 0; r < 24; r++) {
+    uint32_t c[5], rc1[5], b[25];
+#pragma unroll
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    // rotl64(C, 1): the even half is the odd half rotated by 1, the odd half is the even half
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const uint32_t p = k_xchg(c[x]);
+      rc1[x] = __builtin_amdgcn_alignbit(p, p, 31u + h);  // rotl by 1 - h
+    }
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const uint32_t d = c[(x + 4) % 5] ^ rc1[(x + 1) % 5];
+#pragma unroll
+      for (int y = 0; y < 5; y++) a[5 * y + x] ^= d;
+    }
+    // rho + pi: b[pi(i)] = rotl64(a[i], RHO[i])
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+      for (int y = 0; y < 5; y++) {
+        const int i = 5 * y + x, rho = RHO[i], k = rho >> 1;
+        uint32_t v;
+        if ((rho & 1) == 0) {
+          v = rotl32c(a[i], (uint32_t)k);
+        } else {
+          const uint32_t p = k_xchg(a[i]);
+          v = __builtin_amdgcn_alignbit(p, p, (uint32_t)(31 - k) + h);  // rotl by k + 1 - h
+        }
+        b[5 * ((2 * x + 3 * y) % 5) + y] = v;
+      }
+#pragma unroll
+    for (int y = 0; y < 5; y++)
+#pragma unroll
+      for (int x = 0; x < 5; x++) a[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
+    a[0] ^= h ? RCH.o[r] : RCH.e[r];
+  }
+}
+
+__global__ void __launch_bounds__(64) k_merkle_leaves_sha3(const uint8_t* __restrict__ shards, size_t inst_stride,
+                                                           uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
+                                                           const uint16_t* __restrict__ slots, uint32_t nslots) {
+  const uint32_t inst = blockIdx.y, lane = threadIdx.x, h = lane & 1u;
+  uint32_t i = blockIdx.x * 32 + (lane >> 1);
+  if (slots) i = i < nslots ? slots[(size_t)inst * nslots + i] : MERKLE_NO_SLOT;
+  if (i >= n) return;  // whole pairs
+  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)i * L;
+  const uint32_t prefix = i & 0xFF;  // the index byte (plen = 1)
+  const uint64_t total = 1 + (uint64_t)L;
+  const uint64_t nblocks = total / 136 + 1;
+  uint32_t a[25];
+#pragma unroll
+  for (int q = 0; q < 25; q++) a[q] = 0;
+  for (uint64_t blk = 0; blk < nblocks; blk++) {
+    const uint64_t b0 = blk * 136;
+    if (b0 >= 1 && b0 + 136 <= total) {
+      const uint8_t* q = data + (b0 - 1);
+      const uintptr_t ad = (uintptr_t)q;
+      const uint32_t* pa = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(ad & 3);
+      uint32_t d[35];
+#pragma unroll
+      for (int k = 0; k < 34; k++) d[k] = pa[k];
+      d[34] = sh ? pa[34] : 0u;
+#pragma unroll
+      for (int w = 0; w < 17; w++) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * w + 1], d[2 * w], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * w + 2], d[2 * w + 1], sh);
+        a[w] ^= ileave_half(lo, hi, h);
+      }
+    } else {
+#pragma unroll 1
+      for (int w = 0; w < 17; w++) {
+        uint32_t lo = 0, hi = 0;
+        for (int k = 0; k < 8; k++) {
+          const uint64_t pos = b0 + 8 * w + k;
+          uint8_t byte = pos < total ? msg_byte(prefix, 1, data, L, pos) : 0;
+          if (pos == total) byte ^= 0x06;
+          if (blk == nblocks - 1 && 8 * w + k == 135) byte ^= 0x80;
+          if (k < 4) lo |= (uint32_t)byte << (8 * k);
+          else hi |= (uint32_t)byte << (8 * (k - 4));
+        }
+        a[w] ^= ileave_half(lo, hi, h);
+      }
+    }
+    keccak_f1600_il(a, h);
+  }
+  // digest bytes 0..31 = state words 0..3, little-endian; out as 8 big-endian words
+  uint32_t out[8];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const uint32_t mine = a[w], other = k_xchg(a[w]);
+    const uint32_t e = h ? other : mine, o = h ? mine : other;
+    const uint32_t lo = spread16(e) | (spread16(o) << 1);
+    const uint32_t hi = spread16(e >> 16) | (spread16(o >> 16) << 1);
+    out[2 * w] = bswap32(lo);
+    out[2 * w + 1] = bswap32(hi);
+  }
+  if (h == 0) {
+    uint32_t* o = leaf_hash + ((size_t)inst * n + i) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; q++) o[q] = out[q];
+  }
 }
 #endif
 

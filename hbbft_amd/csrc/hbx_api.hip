@@ -417,8 +417,8 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
       hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((n + 63) / 64, inst), dim3(128), 0, s, d_shards, (size_t)n * L,
                          n, L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u);
     else
-      hipLaunchKernelGGL(k_merkle_leaves, dim3((n + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                         c->leaf_hash.as<uint32_t>(), c->merkle, (const uint16_t*)nullptr, 0u);
+      hipLaunchKernelGGL(k_merkle_leaves_sha3, dim3((n + 31) / 32, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n,
+                         L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u);
   }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots, d_nodes,
@@ -918,8 +918,8 @@ static int broadcast_decode(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_pres
         hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((m + 63) / 64, inst), dim3(128), 0, s, d_shards,
                            (size_t)n * L, n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m);
       else
-        hipLaunchKernelGGL(k_merkle_leaves, dim3((m + 63) / 64, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n, L,
-                           c->leaf_hash.as<uint32_t>(), c->merkle, c->leaf_slots.as<uint16_t>(), m);
+        hipLaunchKernelGGL(k_merkle_leaves_sha3, dim3((m + 31) / 32, inst), dim3(64), 0, s, d_shards, (size_t)n * L,
+                           n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m);
     }
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n,

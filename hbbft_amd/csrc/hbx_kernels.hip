@@ -395,9 +395,14 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
     if (skipA && skipB) {
       v = true;
     } else {
-      const fq12d fd = miller_loop2_d(lines[j].h, fqd_from_fq(sh.x), fqd_from_fq(sh.y), !skipA, lines[j].w,
-                                      fqd_from_fq(pki.x), fqd_neg(fqd_from_fq(pki.y)), !skipB);
-      v = fq12d_is_one(final_exponentiation_d(fd, (lds_u32*)(gslots + threadIdx.x)));
+      // the G1 coordinates wait in this lane's LDS slot during the Miller loop (pairingd.hpp)
+      lds_u32* slot = (lds_u32*)(gslots + threadIdx.x);
+      park_put_fqd(slot, 0, fqd_from_fq(sh.x));
+      park_put_fqd(slot, 1, fqd_from_fq(sh.y));
+      park_put_fqd(slot, 2, fqd_from_fq(pki.x));
+      park_put_fqd(slot, 3, fqd_neg(fqd_from_fq(pki.y)));
+      const fq12d fd = miller_loop2_parked_d(lines[j].h, !skipA, lines[j].w, !skipB, slot);
+      v = fq12d_is_one(final_exponentiation_d(fd, slot));
     }
   }
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;

@@ -22,10 +22,11 @@ if [ "${PMC:-0}" = "1" ]; then
   # HBM bytes of one N=256 epoch step: FETCH_SIZE and WRITE_SIZE in separate passes
   R="$GRAFT_REPO_ROOT"
   cd /tmp
-  B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --in-flight 1"
+  B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --in-flight 1 --configs="
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/${tag}_pf" -o run -- python3 -u $B > "$R/gpurun_out/${tag}_pf.log" 2>&1 || { echo "pmc fetch failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/${tag}_pw" -o run -- python3 -u $B > "$R/gpurun_out/${tag}_pw.log" 2>&1 || { echo "pmc write failed"; exit 1; }
   python3 "$R/tools/pmcsum.py" "$R/gpurun_out/${tag}_pf/run_results.db" "$R/gpurun_out/${tag}_pw/run_results.db" > "$R/gpurun_out/${tag}_pmc_hbm.txt" 2>&1 || true
   cat "$R/gpurun_out/${tag}_pmc_hbm.txt"
+  python3 "$R/tools/pmc_json.py" "$R/gpurun_out/${tag}_pf/run_results.db" "$R/gpurun_out/${tag}_pw/run_results.db" "${PMC_KERNEL:-k_verify_shares}" "${COMMIT:-unknown}" > "$R/gpurun_out/${tag}_pmc_hbm.json" && cat "$R/gpurun_out/${tag}_pmc_hbm.json"
 fi
 echo done

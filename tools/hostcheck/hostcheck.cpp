@@ -106,10 +106,18 @@ int hc_miller2_digit_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb
   const fq12 f = miller_loop2(LA, PA, true, LB, PB, true);
   const fq12 g = fq12d_to_fq12(miller_loop2_d(DA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), true, DB,
                                               fqd_from_fq(PB.x), fqd_from_fq(PB.y), true));
+  // the loop with the G1 points parked in the (host: plain) slot gives the same element
+  static uint32_t park[LDS_FQ12D_DWORDS];
+  park_put_fqd(park, 0, fqd_from_fq(PA.x));
+  park_put_fqd(park, 1, fqd_from_fq(PA.y));
+  park_put_fqd(park, 2, fqd_from_fq(PB.x));
+  park_put_fqd(park, 3, fqd_from_fq(PB.y));
+  const fq12 gp = fq12d_to_fq12(miller_loop2_parked_d(DA, true, DB, true, park));
   const fq* a = &f.c0.c0.c0;
   const fq* b = &g.c0.c0.c0;
+  const fq* c = &gp.c0.c0.c0;
   int same = 1;
-  for (int i = 0; i < 12; i++) same &= fq_eq(a[i], b[i]) ? 1 : 0;
+  for (int i = 0; i < 12; i++) same &= (fq_eq(a[i], b[i]) && fq_eq(a[i], c[i])) ? 1 : 0;
   *check = fq12_is_one(final_exponentiation(g)) ? 1 : 0;
   // the digit-form final exponentiation gives the same element as pairing.hpp's
   static uint32_t slot[LDS_FQ12D_DWORDS];

@@ -1,0 +1,39 @@
+"""HBM bytes per launch of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE), as
+the JSON record bench.py's `traffic` field reads (profiles/<tag>_pmc_hbm.json).
+
+    python tools/pmc_json.py <fetch results.db> <write results.db> <kernel> <commit> > out.json
+
+Units and the gfx950 correction follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide reads
+(TCC_EA0_RDREQ x 64 B for 128-B requests), so it is doubled; WRITE_SIZE is taken as is.  Both are
+memory-side (L2 -> fabric) counters, so Infinity-Cache hits are included: an upper bound on HBM
+bytes."""
+import json
+import sqlite3
+import sys
+
+
+def per_launch(db, counter, kernel):
+    c = sqlite3.connect(db)
+    q = ("select sum(value), count(distinct dispatch_id) from counters_collection "
+         "where counter_name = ? and kernel_name like ?")
+    v, nd = c.execute(q, (counter, f"%{kernel}%")).fetchone()
+    if not nd:
+        raise SystemExit(f"no {counter} rows for {kernel} in {db}")
+    return v / nd, nd
+
+
+def main():
+    fdb, wdb, kernel, commit = sys.argv[1:5]
+    f_kib, nf = per_launch(fdb, "FETCH_SIZE", kernel)
+    w_kib, nw = per_launch(wdb, "WRITE_SIZE", kernel)
+    fetch = 2 * f_kib * 1024
+    write = w_kib * 1024
+    print(json.dumps({"kernel": kernel, "bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
+                      "write_bytes": round(write), "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
+                      "launches": [nf, nw], "fetch_correction": 2, "commit": commit,
+                      "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH doubled (gfx950)"}))
+
+
+if __name__ == "__main__":
+    main()
