@@ -629,6 +629,7 @@ def config_c5(args, dev, torch, Context):
                              "traffic": None, "kernel": "k_merkle_leaves" + ("_sha256" if name == "sha256" else "_sha3"),
                              "work": f"{inst} x {n} leaves of {L + 1} B hashed per launch"},
             }
+            variants[name]["node_epoch"] = echo_epoch(ctx, torch, dev, stream, shards, roots, present, k, m, steps)
             if name == "sha256":
                 enc = ms["encode"]
                 dwords = inst * (L // 4)
@@ -647,6 +648,63 @@ def config_c5(args, dev, torch, Context):
     if not args.no_cpu_baseline:
         sub["cpu_baseline"] = cpu_baseline_broadcast(host, k, m, L, payload, roots_by, args.cpu_seconds)
     return sub
+
+
+def echo_epoch(ctx, torch, dev, stream, shards, roots, present, k, m, steps):
+    """One node's Broadcast crypto for a whole epoch (row f3, hbbft_amd/broadcast.py): validate the
+    Echo proof of every (instance, sender) pair -- validate_proof at broadcast.rs:451, one
+    hbx_merkle_validate_d call -- then decode every instance from its validated Echo values with
+    the proofs' leaf digests (hbx_broadcast_decode_leaves_d, compute_output :521-551).  The proofs
+    are MerkleTree::gen_proof outputs of the encoded shards (hbx_merkle_build_d +
+    hbx_merkle_proofs_d, not timed)."""
+    inst, n, L = shards.shape
+    sh = stream.cuda_stream
+    cnt = ctx.merkle_node_count(n)
+    nodes = torch.zeros((inst, cnt, 32), dtype=torch.uint8, device=dev)
+    ctx.merkle_build_d(shards, nodes, stream=sh)
+    P = inst * n
+    req = torch.stack([torch.arange(inst, device=dev).repeat_interleave(n), torch.arange(n, device=dev).repeat(inst)],
+                      dim=1).to(torch.int32).contiguous()
+    nh = torch.zeros((P, 17, 32), dtype=torch.uint8, device=dev)
+    sb = torch.zeros((P, 16, 32), dtype=torch.uint8, device=dev)
+    sides = torch.zeros(P, dtype=torch.int32, device=dev)
+    depth = torch.zeros(P, dtype=torch.int32, device=dev)
+    proot = torch.zeros((P, 32), dtype=torch.uint8, device=dev)
+    ctx.merkle_proofs_d(nodes, n, req, nh, sb, sides, depth, proot, stream=sh)
+    values = torch.empty((P, L + 1), dtype=torch.uint8, device=dev)  # index byte || shard
+    values[:, 0] = torch.arange(n, device=dev).repeat(inst).to(torch.uint8)
+    values[:, 1:] = shards.reshape(P, L)
+    sender = torch.arange(n, device=dev).repeat(inst).to(torch.int32)
+    valid = torch.zeros(P, dtype=torch.uint8, device=dev)
+    leaf = nh.gather(1, depth.long().view(P, 1, 1).expand(P, 1, 32)).view(inst, n, 32).contiguous()
+    work = torch.empty_like(shards)
+    out = torch.zeros((inst, k * L), dtype=torch.uint8, device=dev)
+    out_len = torch.zeros(inst, dtype=torch.int64, device=dev)
+    status = torch.zeros(inst, dtype=torch.int32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tv, td = [], []
+    for s in range(steps + 1):
+        ev[0].record(stream)
+        ctx.merkle_validate_d(values, nh, sb, sides, depth, proot, sender, n, valid, stream=sh)
+        ev[1].record(stream)
+        work.copy_(shards)
+        work[present == 0] = 0xA5
+        ev[2].record(stream)
+        ctx.broadcast_decode_leaves_d(work, present, leaf, roots, k, m, out, out_len, status, stream=sh)
+        ev[3].record(stream)
+        torch.cuda.synchronize(dev)
+        if s:
+            tv.append(ev[0].elapsed_time(ev[1]))
+            td.append(ev[2].elapsed_time(ev[3]))
+    assert bool((valid == 1).all()), "an honest Echo proof failed validate_proof"
+    assert bool((status == 0).all()), "decode of the validated Echo values"
+    vms, dms = float(np.mean(tv)), float(np.mean(td))
+    vbytes = P * (L + 1)
+    return {"echo_proofs": P, "validate_ms": round(vms, 3), "decode_leaves_ms": round(dms, 3),
+            "ms": round(vms + dms, 3), "validate_GBps_hashed": round(vbytes / (vms * 1e-3) / 1e9, 1),
+            "note": f"{P} Echo proofs of {L + 1} B validated in one call + {inst} decodes from the validated "
+                    f"values with their leaf digests ({m - (n - int(present[0].sum().item()))} of {m} spare shards "
+                    f"present per instance)"}
 
 
 def _tree_root(leaf_hashes, node):

@@ -550,7 +550,9 @@ __device__ __forceinline__ void merkle_node(int variant, const uint32_t* l8, con
 // (digest words, big-endian order), by k_merkle_leaves_sha256 / k_merkle_leaves_sha3.  With
 // `slots` (u16[inst][nslots], MERKLE_NO_SLOT = unused) only the listed leaves are hashed: the
 // decode of validated Echo values hashes only the shards it reconstructed (the others' digests
-// come from the Echo proofs, k_import_leaf_hashes).
+// come from the Echo proofs, k_import_leaf_hashes).  With `row` != 0 the rows are proof values
+// of `row` bytes (hbx_merkle_validate_d): leaf i hashes the whole value, its first byte in the
+// prefix position and the other L = row - 1 bytes as the data.
 constexpr uint32_t MERKLE_NO_SLOT = 0xFFFFu;
 
 // SHA-256 Merkle leaves (HBX_MERKLE_SHA256), two waves per 64 leaves of one instance:
@@ -569,7 +571,8 @@ __device__ __forceinline__ uint32_t sha_sig(uint32_t x, int r1, int r2, int r3) 
 #if HBX_IN_TU(6)
 __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __restrict__ shards, size_t inst_stride,
                                                               uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
-                                                              const uint16_t* __restrict__ slots, uint32_t nslots) {
+                                                              const uint16_t* __restrict__ slots, uint32_t nslots,
+                                                              uint32_t row) {
   __shared__ uint4 kw[2][16][64];  // [slot][rounds / 4][lane]
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t inst = blockIdx.y;
@@ -578,8 +581,10 @@ __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __r
   const bool live = i < n;
   // a block with no leaf to hash (all its slots unused) leaves at once, both waves together
   if (!__syncthreads_or(live ? 1 : 0)) return;
-  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)(live ? i : 0) * L;
-  const uint32_t prefix = (i & 0xFF) << 8;  // bytes 0x00, i
+  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)(live ? i : 0) * (row ? row : L);
+  // bytes 0x00, i -- or, for proof values (row != 0: rows of `row` bytes, the data after their
+  // first byte), 0x00, value[0]
+  const uint32_t prefix = (row ? (live ? (uint32_t)data[-1] : 0u) : (i & 0xFF)) << 8;
   const uint64_t total = 2 + (uint64_t)L;
   const uint64_t nblocks = (total + 9 + 63) / 64;
   // producer state: raw dwords of the next block (fast blocks: whole 64 bytes of shard data)
@@ -809,13 +814,14 @@ __device__ __forceinline__ void keccak_f1600_il(uint32_t* a, uint32_t h) {
 
 __global__ void __launch_bounds__(64) k_merkle_leaves_sha3(const uint8_t* __restrict__ shards, size_t inst_stride,
                                                            uint32_t n, uint32_t L, uint32_t* __restrict__ leaf_hash,
-                                                           const uint16_t* __restrict__ slots, uint32_t nslots) {
+                                                           const uint16_t* __restrict__ slots, uint32_t nslots,
+                                                           uint32_t row) {
   const uint32_t inst = blockIdx.y, lane = threadIdx.x, h = lane & 1u;
   uint32_t i = blockIdx.x * 32 + (lane >> 1);
   if (slots) i = i < nslots ? slots[(size_t)inst * nslots + i] : MERKLE_NO_SLOT;
   if (i >= n) return;  // whole pairs
-  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)i * L;
-  const uint32_t prefix = i & 0xFF;  // the index byte (plen = 1)
+  const uint8_t* data = shards + (size_t)inst * inst_stride + (size_t)i * (row ? row : L);
+  const uint32_t prefix = row ? (uint32_t)data[-1] : (i & 0xFF);  // the index byte / value[0] (plen = 1)
   const uint64_t total = 1 + (uint64_t)L;
   const uint64_t nblocks = total / 136 + 1;
   uint32_t a[25];
@@ -1009,7 +1015,8 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
                                                         const uint32_t* __restrict__ depth,
                                                         const uint8_t* __restrict__ root_hash,
                                                         const uint32_t* __restrict__ sender, uint32_t count,
-                                                        uint32_t nproofs, uint8_t* __restrict__ valid, int variant) {
+                                                        uint32_t nproofs, uint8_t* __restrict__ valid, int variant,
+                                                        const uint32_t* __restrict__ vdigest) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nproofs) return;
   const uint32_t d = depth[j];
@@ -1024,7 +1031,12 @@ __global__ void __launch_bounds__(64) k_merkle_validate(const uint8_t* __restric
   };
   uint32_t h[8], want[8], a[8], b[8];
   if (ok) {
-    merkle_leaf_value(variant, val, vlen, h);
+    if (vdigest) {  // the values' leaf digests, hashed beforehand by the leaf kernels
+#pragma unroll
+      for (int q = 0; q < 8; q++) h[q] = vdigest[(size_t)j * 8 + q];
+    } else {
+      merkle_leaf_value(variant, val, vlen, h);
+    }
     be8(nodes + (size_t)d * 32, want);
     for (int q = 0; q < 8; q++) ok = ok && h[q] == want[q];
   }

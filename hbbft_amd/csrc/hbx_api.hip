@@ -87,7 +87,7 @@ struct hbx_ctx {
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
   dbuf gf_log, gf_exp;
   uint32_t rs_k = 0, rs_m = 0;
-  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, leaf_slots, roots;
+  dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, leaf_slots, val_digest, roots;
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
   dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
@@ -415,10 +415,10 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
     timed t_(c, HBX_K_MERKLE_LEAVES, s);
     if (c->merkle == HBX_MERKLE_SHA256)
       hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((n + 63) / 64, inst), dim3(128), 0, s, d_shards, (size_t)n * L,
-                         n, L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u);
+                         n, L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u, 0u);
     else
       hipLaunchKernelGGL(k_merkle_leaves_sha3, dim3((n + 31) / 32, inst), dim3(64), 0, s, d_shards, (size_t)n * L, n,
-                         L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u);
+                         L, c->leaf_hash.as<uint32_t>(), (const uint16_t*)nullptr, 0u, 0u);
   }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n, d_roots, d_nodes,
@@ -468,7 +468,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->S_status, &c->fallback, &c->gslot,
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
                   &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef, &c->rs_enc_ptab, &c->rs_ptab_d, &c->rs_ptab_p,
-                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->leaf_slots, &c->roots,
+                  &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->leaf_slots, &c->val_digest, &c->roots,
                   &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
@@ -845,8 +845,26 @@ int hbx_merkle_validate_d(hbx_ctx* c, const uint8_t* d_values, uint32_t vlen, co
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
   stream_scope ss_{c, s};
+  // long values (Echo proofs of real shards): their leaf digests first, by the leaf kernels (the
+  // producer/consumer SHA-256 or the two-lane SHA3 schedule) instead of one lane per value inside
+  // the path check
+  const uint32_t* vdigest = nullptr;
+  if (vlen > 256) {
+    if (!c->val_digest.ensure((size_t)nproofs * 32))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_merkle_validate_d: out of device memory");
+    timed t_(c, HBX_K_MERKLE_LEAVES, s);
+    if (c->merkle == HBX_MERKLE_SHA256)
+      hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((nproofs + 63) / 64, 1), dim3(128), 0, s, d_values + 1, (size_t)0,
+                         nproofs, vlen - 1, c->val_digest.as<uint32_t>(), (const uint16_t*)nullptr, 0u, vlen);
+    else
+      hipLaunchKernelGGL(k_merkle_leaves_sha3, dim3((nproofs + 31) / 32, 1), dim3(64), 0, s, d_values + 1, (size_t)0,
+                         nproofs, vlen - 1, c->val_digest.as<uint32_t>(), (const uint16_t*)nullptr, 0u, vlen);
+    HIPCHK(c, hipGetLastError());
+    vdigest = c->val_digest.as<uint32_t>();
+  }
   hipLaunchKernelGGL(k_merkle_validate, dim3((nproofs + 63) / 64), dim3(64), 0, s, d_values, vlen,
-                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid, c->merkle);
+                     d_node_hash, d_sib_hash, d_sides, d_depth, d_root, d_sender, count, nproofs, d_valid, c->merkle,
+                     vdigest);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -916,10 +934,10 @@ static int broadcast_decode(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_pres
       timed t_(c, HBX_K_MERKLE_LEAVES, s);
       if (c->merkle == HBX_MERKLE_SHA256)
         hipLaunchKernelGGL(k_merkle_leaves_sha256, dim3((m + 63) / 64, inst), dim3(128), 0, s, d_shards,
-                           (size_t)n * L, n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m);
+                           (size_t)n * L, n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m, 0u);
       else
         hipLaunchKernelGGL(k_merkle_leaves_sha3, dim3((m + 31) / 32, inst), dim3(64), 0, s, d_shards, (size_t)n * L,
-                           n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m);
+                           n, L, c->leaf_hash.as<uint32_t>(), c->leaf_slots.as<uint16_t>(), m, 0u);
     }
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(k_merkle_tree, dim3(inst), dim3(128), 0, s, c->leaf_hash.as<uint32_t>(), n,

@@ -223,94 +223,6 @@ HBX_HD fq12d lds_get_fq12d(const lds_u32* base) {
   }
   return a;
 }
-// ---- Fq12 product with the second operand streamed from the LDS slot --------------------------
-// The exponentiation's r * g with g parked in the lane's slot: g's Fq2 coefficients are unpacked
-// one at a time as the six Fq2 products of each Fq6 Karatsuba need them, and every product is
-// folded at once into the two output accumulators (c0 = X0 Y0 + v X1 Y1, c1 = (X0 + X1)(Y0 + Y1)
-// - X0 Y0 - X1 Y1), so neither g nor an Fq6 intermediate is ever whole in registers and no Fq12
-// crosses a call (fq12d_mul_ni's operands and result went through the scratch stack).
-// acc[j] +/-= term for output coefficient i of an Fq6 product C, or of v C (vsh: index i + 1, xi
-// applied when i = 2); the touched coefficient is carry-normalised at once (term digits are below
-// 2^30 in magnitude).
-HBX_HD void fold_term_d(fq6d& acc, int i, const fq2d& x, bool neg, bool vsh) {
-  const int j = vsh ? (i + 1) % 3 : i;
-  const fq2d v = (vsh && i == 2) ? fq2d_mul_xi(x) : x;
-  fq2d* c = &acc.c0;
-  c[j] = fq2d_norm(neg ? fq2d_sub(c[j], v) : fq2d_add(c[j], v));
-}
-// Fq6 Karatsuba C = a y (fq6d_mul) on accessors a(q), y(q) (normalised Fq2 coefficients), each Fq2
-// product folded into acc0 (sign n0, v-shift v0) and, if acc1, into acc1 (n1, v1)
-template <class A, class Y>
-HBX_HD void fq6d_mul_fold_d(fq6d& acc0, bool n0, bool v0, fq6d* acc1, bool n1, bool v1, A a, Y y) {
-  auto fold = [&](int i, const fq2d& x, bool neg) {
-    fold_term_d(acc0, i, x, neg != n0, v0);
-    if (acc1) fold_term_d(*acc1, i, x, neg != n1, v1);
-  };
-  {
-    const fq2d t0 = fq2d_mul(a(0), y(0));
-    fold(0, t0, false);
-    fold(1, t0, true);
-    fold(2, t0, true);
-  }
-  HBX_SEQ();
-  {
-    const fq2d t1 = fq2d_mul(a(1), y(1));
-    fold(0, fq2d_mul_xi(t1), true);
-    fold(1, t1, true);
-    fold(2, t1, false);
-  }
-  HBX_SEQ();
-  {
-    const fq2d t2 = fq2d_mul(a(2), y(2));
-    const fq2d xt2 = fq2d_mul_xi(t2);
-    fold(0, xt2, true);
-    fold(1, xt2, false);
-    fold(2, t2, true);
-  }
-  HBX_SEQ();
-  fold(0, fq2d_mul_xi(fq2d_mul(fq2d_norm(fq2d_add(a(1), a(2))), fq2d_norm(fq2d_add(y(1), y(2))))), false);
-  HBX_SEQ();
-  fold(1, fq2d_mul(fq2d_norm(fq2d_add(a(0), a(1))), fq2d_norm(fq2d_add(y(0), y(1)))), false);
-  HBX_SEQ();
-  fold(2, fq2d_mul(fq2d_norm(fq2d_add(a(0), a(2))), fq2d_norm(fq2d_add(y(0), y(2)))), false);
-  HBX_SEQ();
-}
-HBX_HD fq2d lds_get_fq2d_packed1(const lds_u32* base, int q);
-// X * g, X reduced in registers, g the reduced value packed in `gslot` (lds_put_fq12d).  Reduced.
-HBX_HD fq12d fq12d_mul_lds(const fq12d& X, const lds_u32* gslot) {
-  auto y = [&](int q) { return lds_get_fq2d_packed1(gslot, q); };
-  const fqd z = fqd_zero();
-  fq6d acc0{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
-  fq6d acc1 = acc0;
-  fq6d_mul_fold_d(acc0, false, false, &acc1, true, false, [&](int q) { return (&X.c0.c0)[q]; }, y);
-  fq6d_mul_fold_d(acc0, false, true, &acc1, true, false, [&](int q) { return (&X.c1.c0)[q]; },
-                  [&](int q) { return y(3 + q); });
-  const fq6d s = fq6d_norm(fq6d_add(X.c0, X.c1));
-  fq6d_mul_fold_d(acc1, false, false, (fq6d*)nullptr, false, false, [&](int q) { return (&s.c0)[q]; },
-                  [&](int q) { return fq2d_norm(fq2d_add(y(q), y(3 + q))); });
-  return fq12d{fq6d_reduce(acc0), fq6d_reduce(acc1)};
-}
-
-// coefficient q (0..5) of a packed Fq12 in a slot: Fq elements 2q, 2q + 1 (13 dwords each)
-HBX_HD fq2d lds_get_fq2d_packed1(const lds_u32* base, int q) {
-  fq2d r;
-  fqd* e = &r.c0;
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    uint32_t w[13];
-#pragma unroll
-    for (int k = 0; k < 13; k++) w[k] = base[((2 * q + h) * 13 + k) * LDS_FQ12_STRIDE];
-#pragma unroll
-    for (int i = 0; i < 13; i++) {
-      const int off = 28 * i, word = off >> 5, sh = off & 31;
-      uint32_t d = w[word] >> sh;
-      if (sh > 4) d |= w[word + 1] << (32 - sh);
-      e[h].d[i] = (int32_t)(d & (uint32_t)DMASK);
-    }
-    e[h].d[13] = (int32_t)w[12];
-  }
-  return r;
-}
 // g^|x| (g reduced, in the cyclotomic subgroup): squaring runs between the one bits of |x|
 // (pairing.hpp cyc_exp_abs_x_lds)
 HBX_HDNI fq12d cyc_exp_abs_x_d(const fq12d& g_in, lds_u32* gslot) {
@@ -321,8 +233,7 @@ HBX_HDNI fq12d cyc_exp_abs_x_d(const fq12d& g_in, lds_u32* gslot) {
   for (int q = 0; q < 6; q++) {
     const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
     r = cyc_sqr_n_d(r, run);
-    HBX_SEQ();
-    if (q < 5) r = fq12d_mul_lds(r, gslot);
+    if (q < 5) r = fq12d_mul_ni(r, lds_get_fq12d(gslot));
   }
   return r;
 }

@@ -111,10 +111,14 @@ def flatten(proofs, senders):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [4, 7, 13, 128])
-def test_merkle_validate(hbx_ctx, n):
-    value = bytes(range(256)) * 3
-    _, leaves, tree = rm.send_shards(value, n)
+@pytest.mark.parametrize("variant", ["sha256", "sha3"])
+@pytest.mark.parametrize("n,size", [(4, 768), (7, 768), (13, 768), (128, 768), (13, 200_003), (128, 1_048_576)])
+def test_merkle_validate(hbx_ctx, n, size, variant):
+    """validate_proof over a batch; values longer than 256 B take the leaf-kernel path (their
+    digests hashed first by k_merkle_leaves_sha256 / _sha3), shorter ones the one-lane path."""
+    _set_merkle(hbx_ctx, variant)
+    value = (bytes(range(256)) * (size // 256 + 1))[:size]
+    _, leaves, tree = rm.send_shards(value, n, variant)
     proofs, senders = [], []
     for i, leaf in enumerate(leaves):
         p = tree.gen_proof(leaf)
@@ -123,8 +127,11 @@ def test_merkle_validate(hbx_ctx, n):
         if i % 3 == 0:                       # wrong sender (node_index check)
             proofs.append(p)
             senders.append((i + 1) % n)
-        if i % 4 == 1:                       # corrupted value byte
+        if i % 4 == 1:                       # corrupted value byte (last, then middle)
             proofs.append(dict(p, value=p["value"][:-1] + bytes([p["value"][-1] ^ 1])))
+            senders.append(i)
+            mid = len(p["value"]) // 2
+            proofs.append(dict(p, value=p["value"][:mid] + bytes([p["value"][mid] ^ 0x10]) + p["value"][mid + 1:]))
             senders.append(i)
         if i % 5 == 2 and len(p["lemma"]) > 1:  # corrupted sibling hash
             lem = list(p["lemma"])
@@ -139,7 +146,7 @@ def test_merkle_validate(hbx_ctx, n):
     valid = torch.zeros(len(proofs), dtype=torch.uint8, device="cuda")
     hbx_ctx.merkle_validate_d(*[dev(a) for a in arrs], n, valid)
     torch.cuda.synchronize()
-    want = [rm.validate_broadcast_proof(p, s, n) for p, s in zip(proofs, senders)]
+    want = [rm.validate_broadcast_proof(p, s, n, variant) for p, s in zip(proofs, senders)]
     assert valid.cpu().numpy().astype(bool).tolist() == want
     assert sum(want) == n
 
