@@ -483,7 +483,8 @@ def config_c4(args, dev, torch, Context):
            "kernels_ms": kern,
            "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
                         "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
-                        "kernel": "k_verify_sig_shares", "kernel_ms": kms,
+                        "kernel": "k_verify_sig_shares2 (two lanes per check: 512 one-lane waves would fill half the chip)",
+                        "kernel_ms": kms,
                         "work": f"{inst * n} checks x {VSIG_FQMUL} Fq-mul (frozen unit V_sig) x {MADS_PER_FQMUL} MAD",
                         "opcount": {"fqmul_per_check": OPCOUNT_VSIG, "frac": round(achieved_op / PEAK_TMAD_S, 4)}}}
     if not args.no_cpu_baseline:

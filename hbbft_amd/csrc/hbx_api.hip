@@ -61,6 +61,7 @@ struct hbx_ctx {
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
   int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1, 2 or 3 lanes per share check
+  int coin_lanes_used = 0;            // lanes per check of the last signature-share launch
   int lanes_used = 0;                 // lanes per check of the last share-check launch
   // era state
   uint32_t n_keys = 0;
@@ -1061,11 +1062,28 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
                      c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>());
   HIPCHK(c, hipGetLastError());
   {
+    // two lanes per check when one lane per check would leave SIMDs idle (a coin round of 256
+    // instances at N = 128 is 512 one-lane waves on 1,024 SIMDs), or when asked for
+    // (hbx_set_verify_lanes 2); one lane otherwise
     timed t_(c, HBX_K_VERIFY_SIG, s);
-    hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
-                       c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
-                       c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
-                       c->coin_valid.as<uint8_t>());
+    const size_t waves1 = (size_t)((n + 63) / 64) * count;
+    const int lanes = c->verify_lanes == 1 || c->verify_lanes == 2 ? c->verify_lanes
+                      : waves1 < (size_t)VERIFY_FILL_WAVES ? 2 : 1;
+    c->coin_lanes_used = lanes;
+    if (lanes == 2) {
+      const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
+      if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
+        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
+      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_H.as<g2a>(),
+                         c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(),
+                         present_bits ? c->coin_present.as<uint8_t>() : nullptr, n, c->coin_valid.as<uint8_t>(),
+                         c->gslot.as<uint32_t>());
+    } else {
+      hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
+                         c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
+                         c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
+                         c->coin_valid.as<uint8_t>());
+    }
   }
   HIPCHK(c, hipGetLastError());
   std::vector<uint8_t> v(m);

@@ -495,6 +495,62 @@ __global__ void __launch_bounds__(64) k_verify_shares2(const g1a* __restrict__ S
 }
 #endif
 
+// B1 on TWO lanes per check (k_verify_sig_shares2): the check's two Miller loops are independent,
+// so lane 2m runs f_A = f_{|x|,H}(pk_i) and lane 2m + 1 runs f_B = f_{|x|,sigma_i}(-g1), each with
+// its lines generated on the fly (pairingd.hpp miller_loop_mixed_d with one pair: the same code on
+// both lanes, different data -- no divergence), then the pair multiplies the two results into the
+// split form f = A0 + A1 w in LDS slot B (pairing2d.hpp op_mul) and runs the two-lane final
+// exponentiation (final_exp2d_is_one, no scratch).  Per lane the Miller loop is ~74 % of the
+// one-lane check's (one pair's lines, the squarings on both lanes), and 32,768 checks fill 1,024
+// waves instead of 512.  Same verdicts as k_verify_sig_shares (common_coin.rs:151).
+#if HBX_IN_TU(7)
+__global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict__ H, const g1a* __restrict__ pk,
+                                                           uint32_t n_keys, const g2a* __restrict__ sig,
+                                                           const int32_t* __restrict__ sig_status,
+                                                           const uint8_t* __restrict__ present, uint32_t n,
+                                                           uint8_t* __restrict__ valid, uint32_t* __restrict__ gslot) {
+  __shared__ uint32_t region[LDS2_DWORDS * 64];
+  const int lane = (int)(threadIdx.x & 63);
+  const bool l1 = (lane & 1) != 0;
+  const uint32_t i = blockIdx.x * 32 + (uint32_t)(lane >> 1);
+  const uint32_t inst = blockIdx.y;
+  if (i >= n) return;  // whole pairs
+  const size_t idx = (size_t)inst * n + i;
+  const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
+  bool v = false;
+  if (res == HBX_SHARE_VALID) {
+    // lane 0: e(pk_i, H); lane 1: e(-g1, sigma_i)
+    g2a Q = l1 ? sig[idx] : H[inst];
+    g1a P;
+    if (l1) {
+      P.x = fq_from_const(G1_GEN_X);
+      P.y = fq_neg(fq_from_const(G1_GEN_Y));
+      P.inf = false;
+    } else {
+      P = pk[i];
+    }
+    const bool use = !(Q.inf || P.inf);  // a pairing with the identity contributes 1
+    const fqd z = fqd_zero();
+    const fq12d f = miller_loop_mixed_d(nullptr, z, z, false, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(P.x),
+                                        fqd_from_fq(P.y), use);
+    lds_u32* reg = (lds_u32*)region;
+    const int pl = lane & ~1;
+    const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
+    uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
+    const slot2<uint32_t*> G1{gb, 64u}, G2{gb + LDS_FQ6D_PACKED * 64, 64u};
+    // each lane parks its whole Fq12 in its slot (A: f_A, B: f_B), both halves
+    const slot2<lds_u32*>& mine = l1 ? B : A;
+    slot_put_fq6d(mine.half(0), mine.stride, fq6d_reduce(f.c0));
+    slot_put_fq6d(mine.half(1), mine.stride, fq6d_reduce(f.c1));
+    HBX_SEQ();
+    op_mul(B, A, false, false, l1);  // B = f_B f_A, lane k its half
+    HBX_SEQ();
+    v = final_exp2d_is_one(A, B, G1, G2, l1);
+  }
+  if (!l1) valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+}
+#endif
+
 constexpr int COMBINE_THREADS = 256;
 constexpr int COMBINE_MAX_T = 4096;
 constexpr int COMBINE_LDS_T = 512;  // Lagrange x_k cached in LDS up to this threshold

@@ -28,10 +28,14 @@ def _nonces(d):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [0, 1, 2])
 @pytest.mark.parametrize("n", [4, 7, 128, "coin_n4_sha3"])
-def test_coin_matches_golden(hbx_ctx, n):
+def test_coin_matches_golden(hbx_ctx, n, lanes):
+    """lanes: the signature-share check on one lane per check, on two (k_verify_sig_shares2), or
+    the automatic choice (two below a full chip: these fixtures)."""
     d = _load(n)
     _digest(hbx_ctx, d)
+    hbx_ctx.set_verify_lanes(lanes)
     assert (hbx_ctx.set_pk_shares([r.tobytes() for r in d["pk_comp"]]) == 0).all()
     h = hbx_ctx.prepare_nonces(_nonces(d))
     np.testing.assert_array_equal(h, d["h"])
