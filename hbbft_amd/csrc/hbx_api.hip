@@ -57,6 +57,8 @@ struct dbuf {
 struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux_stream = nullptr;      // side work of hbx_prepare_nonces (the true H)
+  hipEvent_t aux_ev[2] = {nullptr, nullptr};
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
@@ -91,7 +93,7 @@ struct hbx_ctx {
   dbuf rs_enc, rs_enc_job, rs_enc_coef, rs_enc_ptab, rs_ptab_d, rs_ptab_p, rs_jobs_d, rs_jobs_p, rs_coef_d, rs_coef_p, leaf_hash, leaf_slots, val_digest, roots;
   // common coin state: nonces' hash_g2 points and lines, signature shares, combined signatures
   uint32_t coin_I = 0, coin_n = 0;
-  dbuf coin_blob, coin_off, coin_H, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
+  dbuf coin_blob, coin_off, coin_H, coin_Hp, coin_lines, coin_scratch, coin_sk, coin_sig96, coin_sig, coin_sig_st, coin_present,
       coin_valid, coin_comb, coin_comb_st, coin_mpk_comp, coin_mpk, coin_mpk_st, coin_ok, coin_par, coin_out96;
   // PublicKey::verify batches (hbx_verify_sigs)
   dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_lines_d, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
@@ -470,7 +472,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->shares_own, &c->present_own, &c->keys,     &c->status,    &c->out_own,
                   &c->gf_log,   &c->gf_exp,     &c->rs_enc,      &c->rs_enc_job, &c->rs_enc_coef, &c->rs_enc_ptab, &c->rs_ptab_d, &c->rs_ptab_p,
                   &c->rs_jobs_d, &c->rs_jobs_p, &c->rs_coef_d,   &c->rs_coef_p, &c->leaf_hash, &c->leaf_slots, &c->val_digest, &c->roots,
-                  &c->coin_blob, &c->coin_off,  &c->coin_H,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
+                  &c->coin_blob, &c->coin_off,  &c->coin_H, &c->coin_Hp,      &c->coin_lines, &c->coin_scratch, &c->coin_sk,
                   &c->coin_sig96, &c->coin_sig, &c->coin_sig_st, &c->coin_present, &c->coin_valid, &c->coin_comb,
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
@@ -479,6 +481,9 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipEventDestroy(c->ev_last);
+  if (c->aux_ev[0]) (void)hipEventDestroy(c->aux_ev[0]);
+  if (c->aux_ev[1]) (void)hipEventDestroy(c->aux_ev[1]);
+  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return HBX_OK;
@@ -986,7 +991,8 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   hipStream_t s = pick(c, c->stream);
   stream_scope ss_{c, s};
   if (!c->coin_blob.ensure(total ? total : 16) || !c->coin_off.ensure((size_t)(count + 1) * 8) ||
-      !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
+      !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_Hp.ensure((size_t)count * sizeof(g2a)) ||
+      !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
       !c->coin_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
       !c->coin_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->coin_out96.ensure((size_t)count * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
@@ -995,12 +1001,24 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   {
     timed t_(c, HBX_K_HASH_NONCES, s);
     hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
-                       c->coin_off.as<uint64_t>(), count, c->coin_H.as<g2a>(), c->digest);
+                       c->coin_off.as<uint64_t>(), count, c->coin_Hp.as<g2a>(), c->digest, 0);
   }
   HIPCHK(c, hipGetLastError());
+  // the true H (for hbx_sign and h96) on the auxiliary stream, beside the line preparation
+  if (!c->aux_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+  if (!c->aux_ev[0]) {
+    HIPCHK(c, hipEventCreateWithFlags(&c->aux_ev[0], hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->aux_ev[1], hipEventDisableTiming));
+  }
+  HIPCHK(c, hipEventRecord(c->aux_ev[0], s));
+  HIPCHK(c, hipStreamWaitEvent(c->aux_stream, c->aux_ev[0], 0));
+  hipLaunchKernelGGL(k_h2_from_heff, dim3((count + 63) / 64), dim3(64), 0, c->aux_stream, c->coin_Hp.as<g2a>(), count,
+                     c->coin_H.as<g2a>());
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->aux_ev[1], c->aux_stream));
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count,
+    hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
                        c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                        UINT32_MAX, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
@@ -1009,6 +1027,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
                        c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
   }
   HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamWaitEvent(s, c->aux_ev[1], 0));  // the true H is in
   if (h96) {
     hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count, 1u,
                        c->coin_out96.as<uint8_t>());
@@ -1074,13 +1093,13 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
       const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
       if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
         return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
-      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_H.as<g2a>(),
+      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_Hp.as<g2a>(),
                          c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(),
                          present_bits ? c->coin_present.as<uint8_t>() : nullptr, n, c->coin_valid.as<uint8_t>(),
                          c->gslot.as<uint32_t>());
     } else {
       hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
-                         c->coin_H.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
+                         c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
                          c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
                          c->coin_valid.as<uint8_t>());
     }
@@ -1119,7 +1138,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   HIPCHK(c, hipMemcpyAsync(c->vs_sig96.p, sig96, (size_t)count * 96, hipMemcpyHostToDevice, s));
   // H_i = hash_g2(msg_i) on lane groups, its Miller lines, the signatures' decode
   hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s,
-                     c->vs_blob.as<uint8_t>(), c->vs_off.as<uint64_t>(), count, c->vs_H.as<g2a>(), c->digest);
+                     c->vs_blob.as<uint8_t>(), c->vs_off.as<uint64_t>(), count, c->vs_H.as<g2a>(), c->digest, 1);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_decompress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_sig96.as<uint8_t>(), (size_t)count,
                      c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>());
@@ -1230,7 +1249,7 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   {
     // the G2 combine (blocks y = 0) and the master-key check (y = 1) in one launch
     timed t_(c, HBX_K_COMBINE_SIGS, s);
-    hipLaunchKernelGGL(k_combine_sigs, dim3(I, 2), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
+    hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
                        c->coin_sig.as<g2a>(), c->coin_n, t, c->pk.as<g1a>(), c->coin_mpk.as<g1a>(),
                        c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
   }

@@ -519,12 +519,12 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
   bool v = false;
   if (res == HBX_SHARE_VALID) {
-    // lane 0: e(pk_i, H); lane 1: e(-g1, sigma_i)
+    // lane 0: e(pk_i, H'); lane 1: e(-[m] g1, sigma_i)  (H' = [m] H: the same verdict)
     g2a Q = l1 ? sig[idx] : H[inst];
     g1a P;
     if (l1) {
-      P.x = fq_from_const(G1_GEN_X);
-      P.y = fq_neg(fq_from_const(G1_GEN_Y));
+      P.x = fq_from_const(G1_MGEN_X);
+      P.y = fq_neg(fq_from_const(G1_MGEN_Y));
       P.inf = false;
     } else {
       P = pk[i];
@@ -1027,15 +1027,23 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
 // ----------------------------------------------------------------------------------------------
 #if HBX_IN_TU(5)
 // H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one HASH_K-lane
-// group each.
+// group each.  full = 0: H'_i = h_eff P = [m] H_i (m = 3(x^2 - 1), the decryption checks' trick,
+// DESIGN.md §4.2): the coin's share checks take H' with [m] g1 on the G1 side, and the true H_i
+// (for SecretKeyShare::sign and the API's output) comes from k_h2_from_heff, off the checks' path.
 __global__ void __launch_bounds__(64) k_hash_nonces(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
-                                                    uint32_t count, g2a* __restrict__ H, int digest) {
+                                                    uint32_t count, g2a* __restrict__ H, int digest, int full) {
   const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / HASH_K;
   if (j >= count) return;  // whole groups only
   uint8_t d[32];
   digest2(digest, blob + off[j], off[j + 1] - off[j], nullptr, 0, d);
   g2j h;
-  if (hash_g2_group<HASH_K>(d, true, h)) H[j] = g2_to_affine(h);
+  if (hash_g2_group<HASH_K>(d, true, h, full != 0)) H[j] = g2_to_affine(h);
+}
+// H = h2 P from H' = h_eff P (hash.hpp g2_heff_to_h2), one lane per point
+__global__ void __launch_bounds__(64) k_h2_from_heff(const g2a* __restrict__ Hp, uint32_t count, g2a* __restrict__ H) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  H[j] = Hp[j].inf ? Hp[j] : g2_to_affine(g2_heff_to_h2(g2_from_affine(Hp[j])));
 }
 
 __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict__ comp, size_t count,
@@ -1091,9 +1099,9 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre_d* __re
   const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
   bool v = false;
   if (res == HBX_SHARE_VALID) {
-    g1a ng;
-    ng.x = fq_from_const(G1_GEN_X);
-    ng.y = fq_neg(fq_from_const(G1_GEN_Y));
+    g1a ng;  // -[m] g1 against H' = [m] H
+    ng.x = fq_from_const(G1_MGEN_X);
+    ng.y = fq_neg(fq_from_const(G1_MGEN_Y));
     ng.inf = false;
     v = check_mixed_d(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng,
                       (lds_u32*)(gslots + threadIdx.x));
@@ -1180,13 +1188,13 @@ __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
 // four independent 64-bit scalar multiplications, one per lane (lane 4k + i), instead of one
 // 255-bit multiplication: a quarter of the doubling chain.
 //
-// B3 master check (PublicKey::verify(sig, nonce), common_coin.rs:196) in the same launch, on
-// blocks y = 1: every S_k was verified, e(pk_k, H) = e(g1, S_k), so by bilinearity
+// B3 master check (PublicKey::verify(sig, nonce), common_coin.rs:196) in the same block, on its
+// last wave: every S_k was verified, e(pk_k, H) = e(g1, S_k), so by bilinearity
 //     e(g1, sig) = prod e(g1, S_k)^lambda_k = e(sum lambda_k pk_k, H),
 // and e(master_pk, H) = e(g1, sig)  <=>  sum lambda_k pk_k = master_pk  (H != O, prime order):
 // the same bit as the pairing check, from a G1 Lagrange sum over the same index set (GLV halves
 // on two lanes, 4-bit windows, like k_combine) -- concurrent with the G2 sum instead of a pairing
-// after it.  master_ok = 0 where the combine fails.  One block per (instance, part).
+// after it.  master_ok = 0 where the combine fails.  One block per instance.
 // status: 0 or -3 (NotEnoughShares).
 #endif
 constexpr int SIGCOMB_THREADS = 256;
@@ -1200,13 +1208,16 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
                                                                   const g1a* __restrict__ master_pk,
                                                                   g2a* __restrict__ out, int32_t* __restrict__ status,
                                                                   uint8_t* __restrict__ master_ok) {
+  // One block per instance: waves 0..2 the G2 combine (four psi-digit lanes per share), wave 3 the
+  // G1 master identity (two GLV lanes per share).  At t = 43 that is 172 + 86 tasks on 256 threads
+  // in ONE round of blocks (a block row per part made 512 one-wave-per-SIMD blocks, two rounds).
+  constexpr int G2_THREADS = SIGCOMB_THREADS - 64;
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;
-  __shared__ g2j red2[SIGCOMB_THREADS / 64];
-  __shared__ g1j red1[SIGCOMB_THREADS / 64];
+  __shared__ g2j red2[G2_THREADS / 64];
   const uint32_t inst = blockIdx.x;
-  const bool g1_part = blockIdx.y == 1;
   const int tid = threadIdx.x;
+  const bool g1_part = tid >= G2_THREADS;  // the last wave
   if (tid == 0) {
     int c = 0;
     for (uint32_t i = 0; i < n && c < (int)t; i++)
@@ -1216,64 +1227,56 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
   __syncthreads();
   if (s_count < (int)t) {
     if (tid == 0) {
-      if (g1_part) {
-        master_ok[inst] = 0;
-      } else {
-        status[inst] = -3;
-        out[inst].inf = true;
-      }
+      master_ok[inst] = 0;
+      status[inst] = -3;
+      out[inst].inf = true;
     }
     return;
   }
+  g1j acc1 = g1_identity();
+  g2j acc2 = g2_identity();
   if (g1_part) {
-    g1j acc = g1_identity();
-    for (int q = tid; q < 2 * (int)t; q += SIGCOMB_THREADS) {
+    for (int q = tid - G2_THREADS; q < 2 * (int)t; q += 64) {
       const int k = q >> 1;
       const fr lam = lagrange_at_zero(idx, (int)t, k);
       uint32_t k1[4], k2[4];
       g1_glv_split(lam.l, k1, k2);
       g1a pp = pk[idx[k]];
       if (q & 1) pp.x = fq_mul(pp.x, fq_from_const(G1_BETA));
-      acc = g1_add(acc, g1_mul_u128_w4(pp, (q & 1) ? k2 : k1));
+      acc1 = g1_add(acc1, g1_mul_u128_w4(pp, (q & 1) ? k2 : k1));
     }
 #pragma unroll 1
-    for (int m = 1; m < 64; m <<= 1) acc = g1_add(acc, g1j_shfl_xor(acc, m));
-    if ((tid & 63) == 0) red1[tid >> 6] = acc;
-    __syncthreads();
-    if (tid == 0) {
-      g1j sum = red1[0];
-      for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g1_add(sum, red1[w]);
-      // sum == master_pk (affine, not the identity): X = x Z^2, Y = y Z^3
-      const g1a M = master_pk[0];
-      bool eq = !g1j_is_identity(sum) && !M.inf;
-      if (eq) {
-        const fq zz = fq_sqr(sum.z);
-        eq = fq_eq(sum.x, fq_mul(M.x, zz)) && fq_eq(sum.y, fq_mul(M.y, fq_mul(zz, sum.z)));
-      }
-      master_ok[inst] = eq ? 1 : 0;
+    for (int m = 1; m < 64; m <<= 1) acc1 = g1_add(acc1, g1j_shfl_xor(acc1, m));
+  } else {
+    for (int q = tid; q < 4 * (int)t; q += G2_THREADS) {
+      const int k = q >> 2, i = q & 3;
+      const fr lam = lagrange_at_zero(idx, (int)t, k);
+      uint64_t d[4];
+      fr_base_x_digits(lam.l, d);
+      g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
+      for (int e = 0; e < i; e++) P = g2_psi(P);  // affine in, affine out (Z = 1)
+      g2a Pa{P.x, i & 1 ? fq2_neg(P.y) : P.y, false};
+      if (d[i] != 0) acc2 = g2_add(acc2, g2_mul_u64_naf(Pa, d[i]));
     }
-    return;
-  }
-  g2j acc = g2_identity();
-  for (int q = tid; q < 4 * (int)t; q += SIGCOMB_THREADS) {
-    const int k = q >> 2, i = q & 3;
-    const fr lam = lagrange_at_zero(idx, (int)t, k);
-    uint64_t d[4];
-    fr_base_x_digits(lam.l, d);
-    g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
-    for (int e = 0; e < i; e++) P = g2_psi(P);  // affine in, affine out (Z = 1)
-    g2a Pa{P.x, i & 1 ? fq2_neg(P.y) : P.y, false};
-    if (d[i] != 0) acc = g2_add(acc, g2_mul_u64_naf(Pa, d[i]));
-  }
 #pragma unroll 1
-  for (int m = 1; m < 64; m <<= 1) acc = g2_add(acc, g2j_shfl_xor(acc, m));
-  if ((tid & 63) == 0) red2[tid >> 6] = acc;
+    for (int m = 1; m < 64; m <<= 1) acc2 = g2_add(acc2, g2j_shfl_xor(acc2, m));
+    if ((tid & 63) == 0) red2[tid >> 6] = acc2;
+  }
   __syncthreads();
   if (tid == 0) {
     g2j sum = red2[0];
-    for (int w = 1; w < SIGCOMB_THREADS / 64; w++) sum = g2_add(sum, red2[w]);
+    for (int w = 1; w < G2_THREADS / 64; w++) sum = g2_add(sum, red2[w]);
     out[inst] = g2_to_affine(sum);
     status[inst] = 0;
+  } else if (tid == G2_THREADS) {
+    // the G1 Lagrange sum == master_pk (affine, not the identity): X = x Z^2, Y = y Z^3
+    const g1a M = master_pk[0];
+    bool eq = !g1j_is_identity(acc1) && !M.inf;
+    if (eq) {
+      const fq zz = fq_sqr(acc1.z);
+      eq = fq_eq(acc1.x, fq_mul(M.x, zz)) && fq_eq(acc1.y, fq_mul(M.y, fq_mul(zz, acc1.z)));
+    }
+    master_ok[inst] = eq ? 1 : 0;
   }
 }
 
