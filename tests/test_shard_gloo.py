@@ -118,3 +118,43 @@ def test_gpu_shard_slices(hbx_ctx, world):
     np.testing.assert_array_equal(ss, d["expect_share_status"])
     np.testing.assert_array_equal(cs, d["expect_ct_status"])
     np.testing.assert_array_equal(st, d["expect_status"])
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_gather_world1(hbx_ctx):
+    """The all-gather of shard.py on RCCL (backend "nccl") with the slab on the GPU: a world of one
+    rank (the one GPU of a test box) gathers the N = 64 epoch's result slab computed by the engine,
+    through dist.all_gather_into_tensor itself (not the world == 1 shortcut)."""
+    from hbbft_amd import shard
+
+    d = dict(np.load(FIX, allow_pickle=False))
+    n = int(d["n"])
+    assert (hbx_ctx.set_pk_shares([row.tobytes() for row in d["pk_comp"]]) == 0).all()
+    dev = torch.device("cuda", 0)
+    off = d["v_off"].astype(np.int64)
+    t_valid = torch.zeros(n * n, dtype=torch.uint8, device=dev)
+    t_ct = torch.zeros(n, dtype=torch.uint8, device=dev)
+    t_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    hbx_ctx.decrypt_epoch_d(torch.from_numpy(d["u"]).to(dev), torch.from_numpy(d["v_blob"]).to(dev),
+                            torch.from_numpy(off).to(dev), torch.from_numpy(d["w"]).to(dev), n,
+                            int(np.max(np.diff(off))), torch.from_numpy(d["shares"]).to(dev), n, int(d["t"]),
+                            torch.zeros(max(int(off[-1]), 1), dtype=torch.uint8, device=dev), d_valid=t_valid,
+                            d_ct_valid=t_ct, d_status=t_st,
+                            d_present=torch.from_numpy(d["present"].astype(np.uint8)).to(dev))
+    lay = shard.slab_layout(n, n)
+    slab = torch.zeros(lay["size"], dtype=torch.uint8, device=dev)
+    slab[lay["valid"][0]:lay["valid"][1]] = t_valid
+    slab[lay["ct_valid"][0]:lay["ct_valid"][1]] = t_ct
+    slab[lay["status"][0]:lay["status"][1]] = t_st.view(torch.uint8)
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        out = torch.empty_like(slab)
+        dist.all_gather_into_tensor(out, slab)
+        torch.cuda.synchronize(dev)
+    finally:
+        dist.destroy_process_group()
+    ss, cs, st = shard.assemble(out.cpu().numpy().reshape(1, -1), n, 1)
+    np.testing.assert_array_equal(ss, d["expect_share_status"])
+    np.testing.assert_array_equal(cs, d["expect_ct_status"])
+    np.testing.assert_array_equal(st, d["expect_status"])
