@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--no-own-share", action="store_true",
                     help="run Ciphertext::verify as separate checks instead of through the node's own share")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per config")
-    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3),
+    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3, 6),
                     help="lanes per decryption-share check (0: auto by occupancy)")
     ap.add_argument("--in-flight", type=int, default=2,
                     help="also time this many consecutive epochs in flight at once (one context and stream "
@@ -411,14 +411,16 @@ def config_c2(args, dev, torch, Context):
         eb.check(0)
         kern = eb.kernel_ms()
         ctx.set_timing(False)
+        lanes = ctx.verify_lanes_used()
     ms = elapsed / steps * 1e3
     res = {"workload": f"HoneyBadger node-epoch N={n}: {n * n} decryption-share verifies + {n} Ciphertext::verify + "
                        f"{n} combines (t={ep['t']}) + decrypt, |v|={args.vlen} B",
            "value": round(n * n / (elapsed / steps), 1), "unit": "share verifies/s", "ms_per_epoch": round(ms, 3),
            "epoch_ms_hip_events": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), 3),
            "kernels_ms": kern,
-           "roofline": verify_roofline(n * n, kern["verify_shares"], "k_verify_shares3 (auto: 64 x 64 checks "
-                                       "fill 1/16 of the chip one lane per check)"),
+           "verify_lanes": lanes,
+           "roofline": verify_roofline(n * n, kern["verify_shares"], f"k_verify_shares{lanes if lanes > 1 else ''} "
+                                       "(auto: 64 x 64 checks fill 1/16 of the chip one lane per check)"),
            "note": "latency-bound: 4,096 checks leave most SIMDs idle; the per-proposer chains set the time"}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_dec(ep, args.cpu_seconds)
@@ -878,7 +880,7 @@ def main():
     kern = eb.kernel_ms()
     ctx.set_timing(False)
     lanes = ctx.verify_lanes_used()
-    kname = {1: "k_verify_shares", 2: "k_verify_shares2", 3: "k_verify_shares3"}.get(lanes, "k_verify_shares")
+    kname = {1: "k_verify_shares", 2: "k_verify_shares2", 3: "k_verify_shares3", 6: "k_verify_shares6"}.get(lanes, "k_verify_shares")
     traffic = traffic_record() if (n == 256 and pj == 256) else None
     res = {
         "metric": "BLS12-381 share verifies/sec (node) at N=256; crypto ms per HB epoch",

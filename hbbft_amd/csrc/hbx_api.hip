@@ -503,8 +503,8 @@ int hbx_set_digest(hbx_ctx* c, int variant) {
 }
 
 int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
-  if (!c || lanes < 0 || lanes > 3)
-    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1, 2 or 3, not %d", lanes);
+  if (!c || lanes < 0 || lanes > 6 || lanes == 4 || lanes == 5)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1, 2, 3 or 6, not %d", lanes);
   c->verify_lanes = lanes;
   return HBX_OK;
 }
@@ -731,14 +731,19 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
     if (rc) return rc;
     c->ct_known = true;
   }
-  // share checks: one lane per check when the launch fills the chip (throughput), else three
-  // lanes per check (latency: an epoch shard on one of several GPUs; pairing3.hpp).  The two-lane
+  // share checks: one lane per check when the launch fills the chip (throughput), else six lanes
+  // per check when that still leaves at most one wave per SIMD, else three (latency: an epoch
+  // shard on one of several GPUs; pairing3.hpp / pairing3d.hpp).  The two-lane
   // check (no scratch) measured slower than the one-lane check at N=256 (26.6 vs 24.0 ms,
   // profiles/r03a_bench.json), so it is only used when asked for.
   {
     timed t_(c, HBX_K_VERIFY_SHARES, s);
     const size_t waves1 = (size_t)((n + 63) / 64) * p;
-    const int lanes = c->verify_lanes ? c->verify_lanes : waves1 < (size_t)VERIFY_FILL_WAVES ? 3 : 1;
+    const size_t waves6 = (size_t)((n + G6_PER_WAVE - 1) / G6_PER_WAVE) * p;
+    const int lanes = c->verify_lanes                           ? c->verify_lanes
+                      : waves1 >= (size_t)VERIFY_FILL_WAVES   ? 1
+                      : waves6 <= (size_t)VERIFY_FILL_WAVES   ? 6
+                                                              : 3;
     c->lanes_used = lanes;
     if (lanes == 2) {
       // global slots of the final exponentiation: 2 x 78 dwords per lane of the launch
@@ -751,6 +756,12 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, c->gslot.as<uint32_t>());
     }
+    else if (lanes == 6)
+      hipLaunchKernelGGL(k_verify_shares6, dim3((n + G6_PER_WAVE - 1) / G6_PER_WAVE, p), dim3(64), 0, s,
+                         c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,
+                         c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n,
+                         c->valid.as<uint8_t>(), own ? c->own_me : UINT32_MAX,
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
     else if (lanes == 3)
       hipLaunchKernelGGL(k_verify_shares3, dim3((n + G3_PER_WAVE - 1) / G3_PER_WAVE, p), dim3(64), 0, s,
                          c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys,

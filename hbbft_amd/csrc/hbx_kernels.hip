@@ -718,6 +718,42 @@ __device__ __forceinline__ g1a g1_generator() {
 }
 
 #if HBX_IN_TU(3)
+// k_verify_shares with SIX lanes per share (pairing3d.hpp check2_g6d: the two Miller loops on
+// two triplets side by side): 10 checks per wave.  For launches small enough that twice the
+// three-lane wave count still leaves at most one wave per SIMD (an epoch shard).  Same inputs,
+// outputs and own-share semantics.
+__global__ void __launch_bounds__(64, 1) k_verify_shares6(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
+                                                          const uint8_t* __restrict__ present,
+                                                          const g1a* __restrict__ pk, uint32_t n_keys,
+                                                          const g2a* __restrict__ G2pts,
+                                                          const line_block_d* __restrict__ lines,
+                                                          const uint8_t* __restrict__ ct_ok, uint32_t n,
+                                                          uint8_t* __restrict__ valid, uint32_t me,
+                                                          uint8_t* __restrict__ ct_valid) {
+  const int lane = (int)(threadIdx.x & 63);
+  if (lane >= 6 * G6_PER_WAVE) return;
+  grp3 g;
+  g.gl = lane % 3;
+  g.base = lane - g.gl;
+  const bool second = ((lane / 3) & 1) != 0;
+  const uint32_t i = blockIdx.x * G6_PER_WAVE + (uint32_t)(lane / 6);
+  const uint32_t j = blockIdx.y;
+  if (i >= n) return;  // whole groups
+  const size_t idx = (size_t)j * n + i;
+  const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
+                                     ct_ok[j] != 0);
+  bool v = false;
+  if (res == HBX_SHARE_VALID) {
+    g1a npk = pk[i];
+    npk.y = fq_neg(npk.y);
+    v = check2_g6d(lines[j].h, S[idx], G2pts[2 * j].inf, lines[j].w, npk, G2pts[2 * j + 1].inf, second, g);
+  }
+  if (lane % 6 == 0) {
+    valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+    if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+  }
+}
+
 // SecretKey::public_key (threshold_crypto): pk = g1 * sk, one lane per key.
 __global__ void __launch_bounds__(64) k_public_keys(const uint8_t* __restrict__ sk32, uint32_t n,
                                                     uint8_t* __restrict__ pk48) {

@@ -185,5 +185,55 @@ __device__ __forceinline__ bool check2_g3d(const line_pre_d* LA, const g1a& PA, 
   return is_one3(fq4d_to_fq4(final_exp3d(f, g)), g);
 }
 
+// ---- six lanes per check: the two Miller loops side by side ------------------------------------
+// A 6-lane group is two 3-lane groups: triplet 0 (lanes 0..2) runs the Miller loop of pair A,
+// triplet 1 (lanes 3..5) the loop of pair B, in ONE instruction stream -- each step multiplies by
+// one line per lane, the lane's own pair's (both lines are loaded wave-uniform and selected per
+// lane), so a step costs a squaring and one line instead of a squaring and two.  Then each triplet
+// fetches the other's value (3 lanes away) and both hold f_A f_B; the final exponentiation runs
+// on both (the same instructions; triplet 0's result is used).  ~1/3 of the Miller loop's line
+// products per lane fewer than check2_g3d, on twice the lanes: for launches that leave SIMDs idle
+// at three lanes per check.  Same bits as check2_g3d.
+constexpr int G6_PER_WAVE = 10;  // lanes 60..63 idle
+__device__ __forceinline__ line_pre_d line_d_sel(bool c, const line_pre_d& a, const line_pre_d& b) {
+  line_pre_d r;
+  const int32_t* pa = reinterpret_cast<const int32_t*>(&a);
+  const int32_t* pb = reinterpret_cast<const int32_t*>(&b);
+  int32_t* pr = reinterpret_cast<int32_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(line_pre_d) / 4); i++) pr[i] = c ? pa[i] : pb[i];
+  return r;
+}
+__device__ fq4d miller3d_split(const line_pre_d* LA, const line_pre_d* LB, const fqd& px, const fqd& py, bool use,
+                               bool second, const grp3 g) {
+  fq4d f = g.gl == 0 ? fq4d_one() : fq4d_zero();
+  int k = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = sqr3d(f, g);
+    const int steps = ((BLS_X >> i) & 1) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < steps; s++) {
+      const line_pre_d L = line_d_sel(second, ld_uniform(LB + k), ld_uniform(LA + k));
+      if (use) f = line3d(f, L.c0, fq2d_mul_fq(L.c1, px), py, g);
+      k++;
+    }
+  }
+  f = conj3d(f, g);
+  const int lane = (int)(threadIdx.x & 63);
+  return mul3d(f, fq4d_shfl(f, second ? lane - 3 : lane + 3), g);
+}
+// check2_g3d on a 6-lane group: triplet `second` brings pair B (PB, LB), the other pair A.  The
+// skip flags are group-uniform (both triplets evaluate the same four values).
+__device__ __forceinline__ bool check2_g6d(const line_pre_d* LA, const g1a& PA, bool qa_inf, const line_pre_d* LB,
+                                           const g1a& PB, bool qb_inf, bool second, const grp3 g) {
+  const bool skipA = PA.inf || qa_inf;
+  const bool skipB = PB.inf || qb_inf;
+  if (skipA && skipB) return true;
+  const g1a& P = second ? PB : PA;
+  const fq4d f = miller3d_split(LA, LB, fqd_from_fq(P.x), fqd_from_fq(P.y), second ? !skipB : !skipA, second, g);
+  return is_one3(fq4d_to_fq4(final_exp3d(f, g)), g);
+}
+
 #endif  // __HIPCC__
 }  // namespace hbx

@@ -227,7 +227,7 @@ class Context:
         self._check(self.lib.hbx_set_digest(self.h, variant))
 
     def set_verify_lanes(self, lanes: int):
-        """hbx_set_verify_lanes: 0 auto (default), 1, 2 or 3 lanes per decryption-share check."""
+        """hbx_set_verify_lanes: 0 auto (default), 1, 2, 3 or 6 lanes per decryption-share check."""
         self._check(self.lib.hbx_set_verify_lanes(self.h, lanes))
 
     def verify_lanes_used(self) -> int:

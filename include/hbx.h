@@ -133,12 +133,13 @@ int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launch
  * ------------------------------------------------------------------------------------------- */
 int hbx_set_digest(hbx_ctx* ctx, int variant);
 /* Lanes per decryption-share check (no reference counterpart; results identical): 1 = one lane
- * per check, 2 = a lane pair per check (the Fq12 state split in halves: the throughput kernel
- * when a launch fills the chip), 3 = three cooperating lanes per check (lower latency per check:
- * epoch shards on one of several GPUs), 0 = choose by launch size (default: 2 when one-lane
- * checks would fill >= 1024 waves, else 3). */
+ * per check (the throughput kernel when a launch fills the chip), 2 = a lane pair per check (the
+ * Fq12 state split in halves, no scratch), 3 = three cooperating lanes per check, 6 = six lanes per
+ * check (the two Miller loops on two lane triplets side by side; lowest latency per check), 0 =
+ * choose by launch size (default: 1 when one-lane checks fill >= 1024 waves, else 6 when six-lane
+ * checks fit in 1024 waves, else 3). */
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
-/* Lanes per check the last decryption-share launch used (1, 2 or 3; 0 before any launch). */
+/* Lanes per check the last decryption-share launch used (1, 2, 3 or 6; 0 before any launch). */
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
 int hbx_set_merkle_digest(hbx_ctx* ctx, int variant);
 
