@@ -182,6 +182,26 @@ HBX_HDNI g1j g1_mul_u128_w4(const g1a& P, const uint32_t* k4) {
   return acc;
 }
 
+// k * P for a 64-bit scalar: g1_mul_u128_w4's 4-bit fixed window over 16 windows (60 doublings)
+HBX_HDNI g1j g1_mul_u64_w4(const g1a& P, uint64_t k) {
+  g1j tab[16];
+  tab[0] = g1_identity();
+  tab[1] = g1_from_affine(P);
+#pragma unroll 1
+  for (int i = 2; i < 16; i++) tab[i] = g1_add_mixed_i(tab[i - 1], P);
+  g1j acc = tab[k >> 60];
+  g1j nxt = tab[(k >> 56) & 0xFu];
+#pragma unroll 1
+  for (int w = 14; w >= 0; w--) {
+    const g1j cur = nxt;
+    if (w > 0) nxt = tab[(k >> (4 * (w - 1))) & 0xFu];
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) acc = g1_dbl_i(acc);
+    acc = g1_add_i(acc, cur);
+  }
+  return acc;
+}
+
 // GLV split of a canonical scalar k < r: k = k1 + k2 lambda with lambda = x^2 - 1 (128 bits),
 // k1 = k mod lambda, k2 = k div lambda (< lambda + 2 < 2^128 since r = lambda^2 + lambda + 1).
 // Then k P = k1 P + k2 phi(P), phi(x, y) = (beta x, y).

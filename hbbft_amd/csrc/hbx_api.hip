@@ -67,7 +67,7 @@ struct hbx_ctx {
   int lanes_used = 0;                 // lanes per check of the last share-check launch
   // era state
   uint32_t n_keys = 0;
-  dbuf pk, pk_m, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk (k_scale_keys)
+  dbuf pk, pk_m, pk64, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk, pk64 = [2^64] pk (k_scale_keys)
   // epoch state
   uint32_t p_ct = 0;
   dbuf U, G2pts, Hj, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
@@ -465,7 +465,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
-  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
+  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk64,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback, &c->gslot,
@@ -534,7 +534,7 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
   c->verified_p = 0;
   c->coin_n = 0;
   if (!c->pk.ensure((size_t)n * sizeof(g1a)) || !c->pk_m.ensure((size_t)n * sizeof(g1a)) ||
-      !c->pk_status.ensure((size_t)n * 4) || !c->pk_comp.ensure((size_t)n * 48))
+      !c->pk64.ensure((size_t)n * sizeof(g1a)) || !c->pk_status.ensure((size_t)n * 4) || !c->pk_comp.ensure((size_t)n * 48))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_pk_shares: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->pk_comp.p, pk_comp, (size_t)n * 48, hipMemcpyHostToDevice, c->stream));
   if (n) {
@@ -543,7 +543,7 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
     HIPCHK(c, hipGetLastError());
     // [3(x^2-1)] pk_i: the decryption-share checks' G1 side against H' = h_eff P (k_prepare_ct)
     hipLaunchKernelGGL(k_scale_keys, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->pk.as<g1a>(), n,
-                       c->pk_m.as<g1a>());
+                       c->pk_m.as<g1a>(), c->pk64.as<g1a>());
     HIPCHK(c, hipGetLastError());
   }
   std::vector<int32_t> st(n);
@@ -1258,10 +1258,10 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   HIPCHK(c, hipStreamSynchronize(s));
   if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
   {
-    // the G2 combine (blocks y = 0) and the master-key check (y = 1) in one launch
+    // the G2 combine (waves 0..2) and the master-key identity (wave 3), one block per instance
     timed t_(c, HBX_K_COMBINE_SIGS, s);
     hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
-                       c->coin_sig.as<g2a>(), c->coin_n, t, c->pk.as<g1a>(), c->coin_mpk.as<g1a>(),
+                       c->coin_sig.as<g2a>(), c->coin_n, t, c->pk.as<g1a>(), c->pk64.as<g1a>(), c->coin_mpk.as<g1a>(),
                        c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());

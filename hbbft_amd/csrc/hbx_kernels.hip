@@ -587,6 +587,7 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   __shared__ int wcnt[COMBINE_THREADS / 64];
   __shared__ fr xm[COMBINE_LDS_T];  // Montgomery x_k = idx_k + 1 (t <= COMBINE_LDS_T)
   __shared__ fr nall;               // prod_k x_k
+  __shared__ fr tp[COMBINE_LDS_T];  // its product tree
   __shared__ g1j red[COMBINE_THREADS];
   const uint32_t j = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -624,12 +625,16 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
       x.l[0] = (uint32_t)idx[k] + 1;
       xm[k] = fr_to_mont(x);
     }
+    for (int k = tid; k < (int)t; k += COMBINE_THREADS) tp[k] = xm[k];
     __syncthreads();
-    if (tid == 0) {
-      fr nn = xm[0];
-      for (int k = 1; k < (int)t; k++) nn = fr_mul(nn, xm[k]);
-      nall = nn;
+    // N = prod_k x_k by a product tree (ceil(log2 t) levels instead of t - 1 products on one lane)
+    for (int cnt = (int)t; cnt > 1;) {
+      const int half = (cnt + 1) >> 1;
+      for (int i = tid; i < cnt - half; i += COMBINE_THREADS) tp[i] = fr_mul(tp[i], tp[i + half]);
+      __syncthreads();
+      cnt = half;
     }
+    if (tid == 0) nall = tp[0];
     __syncthreads();
   }
   // two lanes per share (GLV): lane 2k computes k1 S_k, lane 2k+1 computes k2 phi(S_k) with
@@ -640,10 +645,17 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
     const int k = q >> 1;
     fr lam;
     if (lds_lag) {
+      // the denominator x_k prod_{m != k} (x_m - x_k) split over the lane pair of share k (lane 2k
+      // takes m < t/2, lane 2k + 1 the rest), the halves multiplied after one exchange
       const fr xk = xm[k];
-      fr den = xk;
-      for (int m = 0; m < (int)t; m++)
+      const int h = q & 1, m0 = h ? (int)t / 2 : 0, m1 = h ? (int)t : (int)t / 2;
+      fr den = h ? fr_from_const(FR_ONE) : xk;
+      for (int m = m0; m < m1; m++)
         if (m != k) den = fr_mul(den, fr_sub(xm[m], xk));
+      fr other;
+#pragma unroll
+      for (int w = 0; w < 8; w++) other.l[w] = (uint32_t)__shfl_xor((int)den.l[w], 1);
+      den = fr_mul(den, other);
       lam = fr_from_mont(fr_mul(nall, fr_inv(den)));
     } else {
       lam = lagrange_at_zero(idx, (int)t, k);
@@ -1034,10 +1046,17 @@ __global__ void __launch_bounds__(64) k_pair_fallback(const uint8_t* __restrict_
 #if HBX_IN_TU(1)
 // pk_m[i] = [3(x^2-1)] pk_i (once per key set): the G1 side of the share checks against
 // H' = [3(x^2-1)] H (k_prepare_ct).
-__global__ void __launch_bounds__(64) k_scale_keys(const g1a* __restrict__ pk, uint32_t n, g1a* __restrict__ pk_m) {
+// pk64[i] = [2^64] pk_i: the coin combine's master identity splits each 128-bit GLV half of
+// lambda_k into two 64-bit multiplications, of pk_k and of pk64_k (k_combine_sigs).
+__global__ void __launch_bounds__(64) k_scale_keys(const g1a* __restrict__ pk, uint32_t n, g1a* __restrict__ pk_m,
+                                                   g1a* __restrict__ pk64) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   pk_m[i] = g1_to_affine(g1_mul_scalar(g1_from_affine(pk[i]), HEFF_M));
+  g1j q = g1_from_affine(pk[i]);
+#pragma unroll 1
+  for (int d = 0; d < 64; d++) q = g1_dbl(q);
+  pk64[i] = g1_to_affine(q);
 }
 // H_j = hash_g1_g2(U_j, V_j) itself from H'_j = h_eff P (hbx_get_ct_hashes), compressed.
 __global__ void __launch_bounds__(64) k_true_hashes(const g2a* __restrict__ G2pts, const g2j* __restrict__ Hj,
@@ -1241,6 +1260,7 @@ __device__ __forceinline__ g1j g1j_shfl_xor(const g1j& a, int m) {
 __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t* __restrict__ valid,
                                                                   const g2a* __restrict__ sig, uint32_t n, uint32_t t,
                                                                   const g1a* __restrict__ pk,
+                                                                  const g1a* __restrict__ pk64,
                                                                   const g1a* __restrict__ master_pk,
                                                                   g2a* __restrict__ out, int32_t* __restrict__ status,
                                                                   uint8_t* __restrict__ master_ok) {
@@ -1251,6 +1271,7 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;
   __shared__ g2j red2[G2_THREADS / 64];
+  __shared__ fr lam_s[COMBINE_LDS_T];  // lambda_k, once per share (t <= COMBINE_LDS_T)
   const uint32_t inst = blockIdx.x;
   const int tid = threadIdx.x;
   const bool g1_part = tid >= G2_THREADS;  // the last wave
@@ -1269,24 +1290,35 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
     }
     return;
   }
+  // lambda_k once per share, shared by its four G2 digit lanes and its four G1 tasks
+  const bool lds_lam = t <= (uint32_t)COMBINE_LDS_T;
+  if (lds_lam) {
+    for (int k = tid; k < (int)t; k += SIGCOMB_THREADS) lam_s[k] = lagrange_at_zero(idx, (int)t, k);
+    __syncthreads();
+  }
   g1j acc1 = g1_identity();
   g2j acc2 = g2_identity();
   if (g1_part) {
-    for (int q = tid - G2_THREADS; q < 2 * (int)t; q += 64) {
-      const int k = q >> 1;
-      const fr lam = lagrange_at_zero(idx, (int)t, k);
-      uint32_t k1[4], k2[4];
-      g1_glv_split(lam.l, k1, k2);
-      g1a pp = pk[idx[k]];
-      if (q & 1) pp.x = fq_mul(pp.x, fq_from_const(G1_BETA));
-      acc1 = g1_add(acc1, g1_mul_u128_w4(pp, (q & 1) ? k2 : k1));
+    // four 64-bit tasks per share: GLV half h of lambda_k = lo + 2^64 hi, [lo] P_h + [hi] [2^64] P_h
+    // with P_0 = pk_k, P_1 = phi(pk_k) (4t tasks of 60 doublings on the wave's 64 lanes instead of
+    // 2t of 124: the master identity no longer outlasts the G2 sum)
+    for (int q = tid - G2_THREADS; q < 4 * (int)t; q += 64) {
+      const int k = q >> 2, h = (q >> 1) & 1, part = q & 1;
+      const fr lam = lds_lam ? lam_s[k] : lagrange_at_zero(idx, (int)t, k);
+      uint32_t kk[2][4];
+      g1_glv_split(lam.l, kk[0], kk[1]);
+      const uint32_t* kh = kk[h];
+      const uint64_t piece = part ? ((uint64_t)kh[3] << 32 | kh[2]) : ((uint64_t)kh[1] << 32 | kh[0]);
+      g1a pp = part ? pk64[idx[k]] : pk[idx[k]];
+      if (h) pp.x = fq_mul(pp.x, fq_from_const(G1_BETA));
+      if (piece != 0) acc1 = g1_add(acc1, g1_mul_u64_w4(pp, piece));
     }
 #pragma unroll 1
     for (int m = 1; m < 64; m <<= 1) acc1 = g1_add(acc1, g1j_shfl_xor(acc1, m));
   } else {
     for (int q = tid; q < 4 * (int)t; q += G2_THREADS) {
       const int k = q >> 2, i = q & 3;
-      const fr lam = lagrange_at_zero(idx, (int)t, k);
+      const fr lam = lds_lam ? lam_s[k] : lagrange_at_zero(idx, (int)t, k);
       uint64_t d[4];
       fr_base_x_digits(lam.l, d);
       g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
