@@ -62,11 +62,13 @@ struct hbx_ctx {
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
-  int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1, 2 or 3 lanes per share check
+  int verify_lanes = 0;               // hbx_set_verify_lanes: 0 auto, 1, 2, 3 or 6 lanes per share check
+  int combine_lanes = 0;              // hbx_set_combine_lanes: 0 auto, 1 or 4 lanes per Lagrange term
   int coin_lanes_used = 0;            // lanes per check of the last signature-share launch
   int lanes_used = 0;                 // lanes per check of the last share-check launch
   // era state
   uint32_t n_keys = 0;
+  dbuf comb_partial, comb_done;  // k_combine_q: per-block partial sums, per-proposer block counters
   dbuf pk, pk_m, pk64, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk, pk64 = [2^64] pk (k_scale_keys)
   // epoch state
   uint32_t p_ct = 0;
@@ -465,7 +467,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
-  dbuf* bufs[] = {&c->pk,       &c->pk_m,       &c->pk64,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
+  dbuf* bufs[] = {&c->comb_partial, &c->comb_done, &c->pk,       &c->pk_m,       &c->pk64,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback, &c->gslot,
@@ -510,6 +512,13 @@ int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
 }
 
 int hbx_get_verify_lanes_used(const hbx_ctx* c) { return c ? c->lanes_used : 0; }
+
+int hbx_set_combine_lanes(hbx_ctx* c, int lanes) {
+  if (!c || (lanes != 0 && lanes != 1 && lanes != 4))
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_combine_lanes: 0 (auto), 1 or 4, not %d", lanes);
+  c->combine_lanes = lanes;
+  return HBX_OK;
+}
 
 int hbx_set_merkle_digest(hbx_ctx* c, int variant) {
   if (!c || (variant != HBX_MERKLE_SHA256 && variant != HBX_MERKLE_SHA3))
@@ -1304,6 +1313,20 @@ int hbx_combine_decrypt_d(hbx_ctx* c, uint32_t t, uint8_t* d_out_blob, int32_t* 
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_decrypt_d: out of device memory");
   {
     timed t_(c, HBX_K_COMBINE, s);
+    // a quad of lanes per GLV term over one-wave blocks when that still leaves at most one wave per
+    // SIMD (an epoch shard; k_combine_q), else one lane per term in one block per proposer
+    const uint32_t nb = (2 * t + COMBQ_TERMS - 1) / COMBQ_TERMS;
+    const bool quads = c->combine_lanes == 4 ? nb <= 16
+                       : c->combine_lanes == 1 ? false
+                                               : nb <= 16 && (size_t)nb * p <= (size_t)VERIFY_FILL_WAVES;
+    if (quads) {
+      if (!c->comb_partial.ensure((size_t)p * nb * sizeof(g1j)) || !c->comb_done.ensure((size_t)p * 4))
+        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_decrypt_d: out of device memory");
+      HIPCHK(c, hipMemsetAsync(c->comb_done.p, 0, (size_t)p * 4, s));
+      hipLaunchKernelGGL(k_combine_q, dim3(nb, p), dim3(64), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
+                         c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>(),
+                         c->digest, c->comb_partial.as<g1j>(), c->comb_done.as<uint32_t>());
+    } else
     hipLaunchKernelGGL(k_combine, dim3(p), dim3(COMBINE_THREADS), 0, s, c->valid.as<uint8_t>(), c->S.as<g1a>(),
                        c->n_shares, t, c->ct_valid.as<uint8_t>(), c->keys.as<uint32_t>(), c->status.as<int32_t>(),
                        c->digest);

@@ -19,6 +19,7 @@
 #include "pairingd.hpp"
 #include "pairing3d.hpp"
 #include "pairing2d.hpp"
+#include "curve4.hpp"
 #include "wide.hpp"
 
 // Split build (tools/build.py): the kernels compile in groups, one translation unit per group
@@ -552,6 +553,7 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
 #endif
 
 constexpr int COMBINE_THREADS = 256;
+constexpr int COMBQ_TERMS = 16;  // k_combine_q: terms (quads) per one-wave block
 constexpr int COMBINE_MAX_T = 4096;
 constexpr int COMBINE_LDS_T = 512;  // Lagrange x_k cached in LDS up to this threshold
 // threshold_crypto interpolate: lambda_k(0) = prod_{m != k} x_m / (x_m - x_k) over Fr with
@@ -674,6 +676,143 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
   }
   if (tid == 0) {
     const g1a g = g1_to_affine(red[0]);
+    uint8_t comp[48], d[32];
+    g1_compress(g, comp);
+    digest2(digest, comp, 48, nullptr, 0, d);  // hash_bytes seed = DIGEST(compress(g))
+    for (int q = 0; q < 8; q++)
+      keys[(size_t)j * 8 + q] = ((uint32_t)d[4 * q] << 24) | ((uint32_t)d[4 * q + 1] << 16) |
+                                ((uint32_t)d[4 * q + 2] << 8) | d[4 * q + 3];
+    status[j] = 0;
+  }
+}
+
+// k_combine for launches that leave most of the chip idle (an epoch shard: p x 172 terms at
+// t = 86 on 1024 SIMDs): the 2t GLV terms of proposer j spread over COMBQ_TERMS-term one-wave
+// blocks (blockIdx.x), a QUAD of lanes per term (curve4.hpp: the doubling in 3 product rounds, the
+// addition in 5 -- 1.5 instead of 2.0 ms per 128-bit multiplication for a lone wave,
+// profiles/r03l_microbench_combine.txt); each block computes the Lagrange coefficients of its own
+// 8 shares (8 lanes per share), sums its terms, and the last block of the proposer to finish
+// (a device-scope counter) sums the partials and derives the key.  Same index set, the same
+// lambda_k and the same sum as k_combine, so the same keys and statuses.  t <= COMBINE_LDS_T.
+__device__ __forceinline__ g1j g1j_shfl_xor_q(const g1j& a, int m) {
+  g1j r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.x.l[i] = (uint32_t)__shfl_xor((int)a.x.l[i], m);
+    r.y.l[i] = (uint32_t)__shfl_xor((int)a.y.l[i], m);
+    r.z.l[i] = (uint32_t)__shfl_xor((int)a.z.l[i], m);
+  }
+  return r;
+}
+__global__ void __launch_bounds__(64, 1) k_combine_q(const uint8_t* __restrict__ valid, const g1a* __restrict__ S,
+                                                     uint32_t n, uint32_t t, const uint8_t* __restrict__ ct_valid,
+                                                     uint32_t* __restrict__ keys, int32_t* __restrict__ status,
+                                                     int digest, g1j* __restrict__ partial,
+                                                     uint32_t* __restrict__ done) {
+  __shared__ uint16_t idx[COMBINE_LDS_T];
+  __shared__ fr xm[COMBINE_LDS_T];
+  __shared__ uint32_t lk[COMBQ_TERMS / 2][8];
+  const uint32_t j = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+  const int lane = threadIdx.x, s = lane & 3, qd = lane >> 2;
+  // the first t valid senders in index order, 64 per step (as k_combine)
+  int count = 0;
+  for (uint32_t i0 = 0; i0 < n && count < (int)t; i0 += 64) {
+    const uint32_t i = i0 + (uint32_t)lane;
+    const bool ok = i < n && valid[(size_t)j * n + i] == HBX_SHARE_VALID;
+    const uint64_t bal = __ballot(ok);
+    const int pos = count + __popcll(bal & ((1ull << lane) - 1));
+    if (ok && pos < (int)t) idx[pos] = (uint16_t)i;
+    count += __popcll(bal);
+  }
+  const bool ctv = ct_valid[j] == HBX_CT_VALID;
+  if (!ctv || count < (int)t) {
+    if (b == 0 && lane == 0) status[j] = !ctv ? -7 : -3;
+    return;  // every block of the proposer returns here: the counter is untouched
+  }
+  __syncthreads();
+  for (int k = lane; k < (int)t; k += 64) {
+    fr x;
+#pragma unroll
+    for (int q = 0; q < 8; q++) x.l[q] = 0;
+    x.l[0] = (uint32_t)idx[k] + 1;
+    xm[k] = fr_to_mont(x);
+  }
+  __syncthreads();
+  // lambda_k = N / (x_k prod_{m != k} (x_m - x_k)) for this block's shares k = 8b + kk: 8 lanes per
+  // share, each a slice of N's factors and of the denominator's, multiplied across the 8 lanes
+  {
+    const int kk = lane >> 3, part = lane & 7;
+    const int k = (int)(COMBQ_TERMS / 2 * b) + kk;
+    const bool have = k < (int)t;
+    const fr xk = xm[have ? k : 0];
+    fr num = fr_from_const(FR_ONE), den = part == 0 ? xk : fr_from_const(FR_ONE);
+    for (int m = part; m < (int)t; m += 8) {
+      num = fr_mul(num, xm[m]);
+      if (m != k) den = fr_mul(den, fr_sub(xm[m], xk));
+    }
+#pragma unroll
+    for (int w = 1; w < 8; w <<= 1) {
+      fr on, od;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        on.l[q] = (uint32_t)__shfl_xor((int)num.l[q], w);
+        od.l[q] = (uint32_t)__shfl_xor((int)den.l[q], w);
+      }
+      num = fr_mul(num, on);
+      den = fr_mul(den, od);
+    }
+    if (have && part == 0) {
+      const fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
+      uint32_t k1[4], k2[4];
+      g1_glv_split(lam.l, k1, k2);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        lk[kk][q] = k1[q];
+        lk[kk][4 + q] = k2[q];
+      }
+    }
+  }
+  __syncthreads();
+  // one term per quad: GLV half h of share k, lambda_k's half times S_k (h = 0) or phi(S_k)
+  const int term = (int)(COMBQ_TERMS * b) + qd;
+  g1j acc = g1_identity();
+  if (term < 2 * (int)t) {
+    const int k = term >> 1, h = term & 1;
+    uint32_t kh[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) kh[q] = lk[k - COMBQ_TERMS / 2 * (int)b][4 * h + q];
+    g1a sp = S[(size_t)j * n + idx[k]];
+    if (h) sp.x = fq_mul(sp.x, fq_from_const(G1_BETA));
+    acc = g1_mul_u128_w4_q4(sp, kh, s);
+  }
+  // the block's 16 quads: butterfly over quads (lane xor 4, 8, 16, 32), every quad ends with the sum
+#pragma unroll 1
+  for (int m = 4; m < 64; m <<= 1) acc = g1_add_q4(acc, g1j_shfl_xor_q(acc, m), s);
+  __shared__ uint32_t last;
+  if (lane == 0) {
+    partial[(size_t)j * nb + b] = acc;
+    __threadfence();
+    last = atomicAdd(&done[j], 1u) == nb - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // the last block of proposer j: the nb partials, a quad each, by the same butterfly
+  g1j tot = g1_identity();
+  if (qd < (int)nb) {
+    const volatile g1j* vp = partial + (size_t)j * nb + qd;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      tot.x.l[i] = vp->x.l[i];
+      tot.y.l[i] = vp->y.l[i];
+      tot.z.l[i] = vp->z.l[i];
+    }
+  }
+#pragma unroll 1
+  for (int m = 4; m < 64; m <<= 1) tot = g1_add_q4(tot, g1j_shfl_xor_q(tot, m), s);
+  if (lane == 0) {
+    done[j] = 0;  // ready for the next launch
+    const g1a g = g1_to_affine(tot);
     uint8_t comp[48], d[32];
     g1_compress(g, comp);
     digest2(digest, comp, 48, nullptr, 0, d);  // hash_bytes seed = DIGEST(compress(g))

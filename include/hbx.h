@@ -141,6 +141,11 @@ int hbx_set_digest(hbx_ctx* ctx, int variant);
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
 /* Lanes per check the last decryption-share launch used (1, 2, 3 or 6; 0 before any launch). */
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
+/* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
+ * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over
+ * one-wave blocks (k_combine_q, t <= 128), 0 = by launch size (default: 4 when the quad blocks fit
+ * in 1024 waves, else 1). */
+int hbx_set_combine_lanes(hbx_ctx* ctx, int lanes);
 int hbx_set_merkle_digest(hbx_ctx* ctx, int variant);
 
 /* ---------------------------------------------------------------------------------------------

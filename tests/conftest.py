@@ -30,4 +30,5 @@ def _default_digests(request):
         ctx.set_digest(0)
         ctx.set_merkle_digest(0)
         ctx.set_verify_lanes(0)
+        ctx.set_combine_lanes(0)
     yield

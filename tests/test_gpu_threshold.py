@@ -292,6 +292,21 @@ def test_decrypt_shares_match_oracle(hbx_ctx, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n7", "hb_epoch_n64", "hb_cols_n256"])
+def test_one_lane_combine_matches_golden(hbx_ctx, name):
+    """The fixtures' launches are small, so the default path runs the quad combine (k_combine_q);
+    this forces the one-lane-per-term combine (k_combine: what a full N = 256 epoch on one GPU
+    uses) through the same plaintext and status expectations."""
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
+    hbx_ctx.set_combine_lanes(1)
+    try:
+        _device_epoch(hbx_ctx, d, own=False)
+    finally:
+        hbx_ctx.set_combine_lanes(0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lanes", [1, 2, 3])
 @pytest.mark.parametrize("name", ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256",
                                   "hb_epoch_n7_sha3"])
