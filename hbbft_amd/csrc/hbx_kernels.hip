@@ -248,6 +248,55 @@ __device__ __forceinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq
   T = g2j{X3, fq2_sub(EG, C8), Z3};
 }
 
+// line_add_step (pairing.hpp) on the LINE_K lanes of a group that all hold T and Q: its Fq
+// products as five rounds of independent products, one per lane (hash.hpp round16), instead of
+// ~60 dependent products on every lane (57.6 us per step, profiles/r03l_microbench_lines.txt).
+// Same values as line_add_step: num = Y - yQ Z^3, den = Z (X - xQ Z^2), c0 = num xQ - yQ den,
+// c1 = -num, c2 = den; T <- T + Q (madd-2007-bl).
+__device__ __forceinline__ void line_add_step_group(g2j& T, const g2a& Q, fq2& c0, fq2& c1, fq2& c2, int gl) {
+  round16 R;
+  r16_clear(R);
+  // round 1: Z1Z1 = Z^2 (0, 1), yQ Z (2..5)
+  r16_sqr(R, 0, T.z);
+  r16_mul(R, 2, Q.y, T.z);
+  fq r = r16_run(R, gl);
+  const fq2 Z1Z1 = r16_get_sqr<0>(r), YqZ = r16_get_mul<2>(r);
+  // round 2: U2 = xQ Z1Z1 (0..3), S2 = yQ Z Z1Z1 (4..7)
+  r16_mul(R, 0, Q.x, Z1Z1);
+  r16_mul(R, 4, YqZ, Z1Z1);
+  r = r16_run(R, gl);
+  const fq2 U2 = r16_get_mul<0>(r), S2 = r16_get_mul<4>(r);
+  const fq2 H = fq2_sub(U2, T.x);  // -(X - xQ Z^2)
+  const fq2 num = fq2_sub(T.y, S2);
+  const fq2 rr = fq2_dbl(fq2_sub(S2, T.y));
+  // round 3: Z H (0..3), HH = H^2 (4, 5), num xQ (6..9), rr^2 (10, 11), (Z + H)^2 (12, 13)
+  r16_mul(R, 0, T.z, H);
+  r16_sqr(R, 4, H);
+  r16_mul(R, 6, num, Q.x);
+  r16_sqr(R, 10, rr);
+  r16_sqr(R, 12, fq2_add(T.z, H));
+  r = r16_run(R, gl);
+  const fq2 den = fq2_neg(r16_get_mul<0>(r));
+  const fq2 HH = r16_get_sqr<4>(r), NX = r16_get_mul<6>(r), RR = r16_get_sqr<10>(r), ZHs = r16_get_sqr<12>(r);
+  const fq2 I = fq2_dbl(fq2_dbl(HH));
+  c1 = fq2_neg(num);
+  c2 = den;
+  // round 4: yQ den (0..3), J = H I (4..7), V = X I (8..11)
+  r16_mul(R, 0, Q.y, den);
+  r16_mul(R, 4, H, I);
+  r16_mul(R, 8, T.x, I);
+  r = r16_run(R, gl);
+  const fq2 YD = r16_get_mul<0>(r), J = r16_get_mul<4>(r), V = r16_get_mul<8>(r);
+  c0 = fq2_sub(NX, YD);
+  const fq2 X3 = fq2_sub(fq2_sub(RR, J), fq2_dbl(V));
+  // round 5: rr (V - X3) (0..3), Y J (4..7)
+  r16_mul(R, 0, rr, fq2_sub(V, X3));
+  r16_mul(R, 4, T.y, J);
+  r = r16_run(R, gl);
+  const fq2 Y3 = fq2_sub(r16_get_mul<0>(r), fq2_dbl(r16_get_mul<4>(r)));
+  T = g2j{X3, Y3, fq2_sub(fq2_sub(ZHs, Z1Z1), HH)};
+}
+
 // g2_raw_lines on a lane group; group lane 0 writes the lines.
 __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int gl, int gbase) {
   g2j T = g2_from_affine(Q);
@@ -262,7 +311,7 @@ __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int 
     }
     k++;
     if ((BLS_X >> i) & 1) {
-      line_add_step(T, Q, c0, c1, c2);
+      line_add_step_group(T, Q, c0, c1, c2, gl);
       if (gl == 0) {
         out[k].c0 = c0;
         out[k].c1 = c1;
