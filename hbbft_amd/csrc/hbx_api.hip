@@ -643,7 +643,9 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     timed t_(c, HBX_K_PREPARE_LINES, s);
     const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
     const bool own_entry = m_early && me_early != UINT32_MAX;
-    hipLaunchKernelGGL(k_prepare_lines, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
+    // grouped addition steps only for small launches (an epoch shard): see g2_raw_lines_group
+    auto kpl = p <= 64 ? k_prepare_lines<true> : k_prepare_lines<false>;
+    hipLaunchKernelGGL(kpl, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
                        own ? c->own_S.as<g1a>() : nullptr, early_n, me_early,
@@ -1038,7 +1040,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
   HIPCHK(c, hipEventRecord(c->aux_ev[1], c->aux_stream));
   {
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
+    hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
                        c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                        UINT32_MAX, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
@@ -1163,7 +1165,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   hipLaunchKernelGGL(k_decompress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_sig96.as<uint8_t>(), (size_t)count,
                      c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>());
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_prepare_lines, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
+  hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
                      c->vs_lines.as<line_pre>(), c->vs_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                      UINT32_MAX, nullptr, nullptr, nullptr);
   HIPCHK(c, hipGetLastError());

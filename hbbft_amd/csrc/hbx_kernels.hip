@@ -297,7 +297,11 @@ __device__ __forceinline__ void line_add_step_group(g2j& T, const g2a& Q, fq2& c
   T = g2j{X3, Y3, fq2_sub(fq2_sub(ZHs, Z1Z1), HH)};
 }
 
-// g2_raw_lines on a lane group; group lane 0 writes the lines.
+// g2_raw_lines on a lane group; group lane 0 writes the lines.  GADD: the addition steps as grouped
+// rounds (line_add_step_group) -- lower latency, but the kernel's register footprint grows and a
+// concurrent epoch's full-chip share checks then overlap it worse (two N = 256 epochs in flight:
+// 28.2 -> 32.5 ms per epoch), so only small launches use it (hbx_api.hip).
+template <bool GADD>
 __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int gl, int gbase) {
   g2j T = g2_from_affine(Q);
   int k = 0;
@@ -311,7 +315,8 @@ __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int 
     }
     k++;
     if ((BLS_X >> i) & 1) {
-      line_add_step_group(T, Q, c0, c1, c2, gl);
+      if (GADD) line_add_step_group(T, Q, c0, c1, c2, gl);
+      else line_add_step(T, Q, c0, c1, c2);
       if (gl == 0) {
         out[k].c0 = c0;
         out[k].c1 = c1;
@@ -326,6 +331,7 @@ __device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int 
 // k_normalise_lines.  With `dec_st` (ciphertext points), the group of point 2j also
 // settles ct_ok[j]: U_j and W_j must decode (threshold_crypto deserialisation); otherwise H_j is
 // replaced by the identity and the proposer's checks are gated off.
+template <bool GADD>
 __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
                                                       line_pre* __restrict__ lines, fq2* __restrict__ scratch,
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
@@ -384,8 +390,12 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
     }
     return;
   }
-  g2_raw_lines_group(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES, gl, gbase);
+  g2_raw_lines_group<GADD>(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES, gl, gbase);
 }
+template __global__ void k_prepare_lines<true>(g2a*, uint32_t, line_pre*, fq2*, const int32_t*, uint32_t, uint8_t*,
+                                               const g1j*, g1a*, uint32_t, uint32_t, g1a*, int32_t*, const g2j*);
+template __global__ void k_prepare_lines<false>(g2a*, uint32_t, line_pre*, fq2*, const int32_t*, uint32_t, uint8_t*,
+                                                const g1j*, g1a*, uint32_t, uint32_t, g1a*, int32_t*, const g2j*);
 
 // Second half of the line preparation: one lane per raw line, (c0, c1) /= c2.  68 independent
 // Fq2 inversions replace the batched inversion (3 x 68 Fq2 products plus one inversion) that
