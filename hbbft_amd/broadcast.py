@@ -187,6 +187,10 @@ class GpuBroadcastEngine:
             lens = {len(v) for v in vals if v is not None}
             if len(lens) != 1 or 0 in lens:
                 continue  # rse: IncorrectShardSize / EmptyShard (or nothing present) -> None
+            if 1 in lens:
+                # leaves that are only the index byte: reconstruct and the tree rebuild may run, but
+                # the glued data has k * 0 < 4 bytes, so glue_shards returns None (broadcast.rs:697-707)
+                continue
             groups.setdefault(lens.pop(), []).append(q)
         for vlen, idx in sorted(groups.items()):
             L = vlen - 1  # the index byte is implied by the position (validate_proof checked it)

@@ -9,6 +9,7 @@
 // column) and the integer VALU for SHA-256 (64 rounds per 64-byte block); no MFMA.
 #pragma once
 #include "hash.hpp"
+#include "dpp.hpp"
 #ifndef HBX_IN_TU
 #define HBX_IN_TU(n) 1  // single-TU build (hbx_kernels.hip defines the split)
 #endif
@@ -768,9 +769,11 @@ struct keccak_rc_halves {
     }
   }
 };
-// Keccak-f[1600] on this lane's halves a[5 y + x]
+// Keccak-f[1600] on this lane's halves a[5 y + x]; both lanes of every active pair active (the
+// swaps are DPP moves: dpp.hpp), checked once per permutation
 __device__ __forceinline__ void keccak_f1600_il(uint32_t* a, uint32_t h) {
   constexpr keccak_rc_halves RCH{};
+  dpp_guard_pairs();
   constexpr int RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
 #pragma unroll
   for (int r = 0; r < 24; r++) {
@@ -863,6 +866,7 @@ __global__ void __launch_bounds__(64) k_merkle_leaves_sha3(const uint8_t* __rest
   }
   // digest bytes 0..31 = state words 0..3, little-endian; out as 8 big-endian words
   uint32_t out[8];
+  dpp_guard_pairs();
 #pragma unroll
   for (int w = 0; w < 4; w++) {
     const uint32_t mine = a[w], other = k_xchg(a[w]);

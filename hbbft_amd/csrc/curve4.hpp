@@ -14,6 +14,7 @@
 // holds the same values, so data-dependent branches are).
 #pragma once
 #include "curve.hpp"
+#include "dpp.hpp"
 
 namespace hbx {
 #if defined(__HIPCC__)
@@ -22,6 +23,7 @@ namespace hbx {
 template <int K>
 __device__ __forceinline__ fq fq_from_quad(const fq& v) {
   static_assert(K >= 0 && K < 4, "quad lane");
+  dpp_guard_src<4, K>();
   fq r;
 #pragma unroll
   for (int i = 0; i < 12; i++)

@@ -10,6 +10,7 @@
 //    lift, multiply by the full cofactor h2, retry).
 #pragma once
 #include "curve.hpp"
+#include "dpp.hpp"
 
 namespace hbx {
 
@@ -318,6 +319,7 @@ __device__ __forceinline__ fq fq_from_lane(const fq& v, int src) {
 template <int K>
 __device__ __forceinline__ fq fq_from_row(const fq& v) {
   static_assert(K >= 0 && K < 16, "row lane");
+  dpp_guard_src<16, K>();
   fq r;
 #pragma unroll
   for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.l[i], 0x150 + K, 0xf, 0xf, false);

@@ -30,6 +30,7 @@
 // Control flow is pair-uniform; every exchange reads the partner lane of the same pair.
 #pragma once
 #include "pairingd.hpp"
+#include "dpp.hpp"
 
 namespace hbx {
 #if defined(__HIPCC__)
@@ -43,6 +44,7 @@ __device__ __forceinline__ T xchg_t(const T& a) {
   T r;
   const int32_t* pa = reinterpret_cast<const int32_t*>(&a);
   int32_t* pr = reinterpret_cast<int32_t*>(&r);
+  dpp_guard_pairs();
 #pragma unroll
   for (int i = 0; i < (int)(sizeof(T) / 4); i++) pr[i] = xchg_i32(pa[i]);
   return r;
@@ -636,6 +638,7 @@ __device__ __forceinline__ bool is_one2d(const fq6d& A, bool l1) {
   const fq6 a = fq6d_to_fq6(A);
   const bool c0ok = l1 ? fq2_is_zero(a.c0) : (fq_eq(a.c0.c0, fq_one()) && fq_is_zero(a.c0.c1));
   const bool mine = c0ok && fq2_is_zero(a.c1) && fq2_is_zero(a.c2);
+  dpp_guard_pairs();
   return mine && xchg_i32(mine ? 1 : 0) != 0;
 }
 

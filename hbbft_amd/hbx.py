@@ -522,7 +522,17 @@ class Context:
                                   d_status, stream=None):
         """hbx_broadcast_decode_leaves_d: d_leaf_hash uint8[inst, k + m, 32] = the present shards'
         leaf digests from their validated Echo proofs."""
+        import torch
+
         inst, n, L = d_shards.shape
+        # k_import_leaf_hashes reads inst * (k + m) * 32 bytes from this pointer, and the root check
+        # trusts them: the layout must be exactly that
+        if n != k + m:
+            raise ValueError(f"broadcast_decode_leaves_d: {n} shards per instance != k + m = {k + m}")
+        if (tuple(d_leaf_hash.shape) != (inst, n, 32) or d_leaf_hash.dtype != torch.uint8
+                or not d_leaf_hash.is_contiguous()):
+            raise ValueError(f"broadcast_decode_leaves_d: d_leaf_hash must be contiguous uint8[{inst}, {n}, 32], "
+                             f"got {d_leaf_hash.dtype}{list(d_leaf_hash.shape)}")
         self._check(self.lib.hbx_broadcast_decode_leaves_d(
             self.h, d_shards.data_ptr(), d_present.data_ptr(), d_leaf_hash.data_ptr(), d_root.data_ptr(), inst, k, m,
             L, d_out.data_ptr(), d_out.shape[1], d_out_len.data_ptr(), d_status.data_ptr(), self._stream(stream)))

@@ -99,8 +99,10 @@ def _tree(shards, variant):
     return leaves, rm.MerkleTree(leaves, variant)
 
 
-def epoch_scenario(n: int, me: int, seed: int, variant: str = "sha256"):
-    """One node's receive log for all n instances of an epoch (n >= 7)."""
+def epoch_scenario(n: int, me: int, seed: int, variant: str = "sha256", short_leaves: int = None):
+    """One node's receive log for all n instances of an epoch (n >= 7).  ``short_leaves``: that
+    proposer (>= 7) sends a valid tree whose leaves are only the index byte (a Byzantine proposal
+    every state machine accepts; its decode glues fewer than 4 bytes and yields nothing)."""
     assert n >= 7
     rng = random.Random(seed)
     f = (n - 1) // 3
@@ -120,6 +122,9 @@ def epoch_scenario(n: int, me: int, seed: int, variant: str = "sha256"):
     sh3 = [bytes(s) for s in rm.send_shards(values[3], n, variant)[0]]
     sh3[1] = sh3[1] + b"\x00"
     trees[3] = _tree(sh3, variant)
+    if short_leaves is not None:
+        assert 7 <= short_leaves < n and short_leaves != me
+        trees[short_leaves] = _tree([b""] * n, variant)
     # proposer 4 equivocates: a second tree (another value) for the nodes >= n - f
     _, leaves4b, tree4b = rm.send_shards(b"equivocation" * 7, n, variant)
 

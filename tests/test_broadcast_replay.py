@@ -76,6 +76,22 @@ def test_replay_logic_epoch(n, me, seed, variant):
     assert res.engine_decodes <= len(node.decode_attempts)
 
 
+SHORT_CASES = [(10, 9, 5, 8), (13, 5, 6, 11)]  # (n, me, seed, proposer with 1-byte leaves)
+
+
+@pytest.mark.parametrize("variant", ["sha256", "sha3"])
+@pytest.mark.parametrize("n,me,seed,short", SHORT_CASES)
+def test_replay_logic_short_leaves(n, me, seed, short, variant):
+    """A proposer whose leaves are only the index byte: proofs validate, Echo and Ready go out, the
+    decode yields nothing (glue_shards: < 4 bytes) and the node stays undecided -- no error."""
+    events, _ = epoch_scenario(n, me, seed, variant, short_leaves=short)
+    node = ob.BroadcastNode(n, me, variant).run(events)
+    res = BroadcastReplay(OracleEngine(variant), n, me).run(events)
+    check_against_oracle(res, node, n)
+    assert any(p == short for p, _, _ in node.decode_attempts)
+    assert short not in {p for p, _ in node.outputs}
+
+
 # ---- GPU --------------------------------------------------------------------------------------
 def _gpu_engine(ctx, variant):
     from hbbft_amd.broadcast import GpuBroadcastEngine
@@ -105,6 +121,16 @@ def test_gpu_replay_epoch(hbx_ctx, n, me, seed, variant):
     res = BroadcastReplay(_gpu_engine(hbx_ctx, variant), n, me).run(events)
     check_against_oracle(res, node, n)
     assert res.engine_decodes <= len(node.decode_attempts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["sha256", "sha3"])
+@pytest.mark.parametrize("n,me,seed,short", SHORT_CASES)
+def test_gpu_replay_short_leaves(hbx_ctx, n, me, seed, short, variant):
+    events, _ = epoch_scenario(n, me, seed, variant, short_leaves=short)
+    node = ob.BroadcastNode(n, me, variant).run(events)
+    res = BroadcastReplay(_gpu_engine(hbx_ctx, variant), n, me).run(events)
+    check_against_oracle(res, node, n)
 
 
 @pytest.mark.gpu

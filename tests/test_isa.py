@@ -1,0 +1,68 @@
+"""Static checks of the shipped gfx950 code (no GPU needed).
+
+* No non-kernel function of libhbx.so makes a far branch through its own return address
+  s[30:31] (tools/isa_check.py: the compiler defect behind the hung builds of rounds 2 and 3 --
+  the function's return jumped back into its own loop).  The check is pinned on a listing
+  shaped like the hung build's, so a silent parser change cannot make it pass vacuously.
+* Every DPP exchange helper carries its EXEC guard (hbbft_amd/csrc/dpp.hpp): the built code
+  holds the trap instructions of those guards.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import isa_check  # noqa: E402
+
+LIB = os.path.join(ROOT, "hbbft_amd", "libhbx.so")
+HUNG_SHAPE = """
+0000000000001000 <_ZN3hbx15cyc_exp_abs_x_dE>:
+\ts_add_i32 s58, s58, 1                                      // 000000001000: 813A813A
+\ts_cbranch_scc0 6                                           // 000000001004: BF840006
+\ts_getpc_b64 s[30:31]                                       // 000000001008: BE9E1C00
+\ts_add_u32 s30, s30, 0x3cdec                                // 00000000100C: 801EFF1E 0003CDEC
+\ts_addc_u32 s31, s31, 0                                     // 000000001014: 821FFF1F 00000000
+\ts_setpc_b64 s[30:31]                                       // 00000000101C: BE801D1E
+\ts_waitcnt vmcnt(0)                                         // 000000001020: BF8C0F70
+\ts_setpc_b64 s[30:31]                                       // 000000001024: BE801D1E
+
+0000000000002000 <_ZN3hbx8k_kernelE>:
+\ts_getpc_b64 s[30:31]                                       // 000000002000: BE9E1C00
+\ts_add_u32 s30, s30, 0x3cdec                                // 000000002004: 801EFF1E 0003CDEC
+\ts_addc_u32 s31, s31, 0                                     // 00000000200C: 821FFF1F 00000000
+\ts_setpc_b64 s[30:31]                                       // 000000002014: BE801D1E
+\ts_endpgm                                                   // 000000002018: BF810000
+
+0000000000003000 <_ZN3hbx10fq_mul_niE>:
+\ts_getpc_b64 s[4:5]                                         // 000000003000: BE841C00
+\ts_add_u32 s4, s4, 0x3cdec                                  // 000000003004: 8004FF04 0003CDEC
+\ts_addc_u32 s5, s5, 0                                       // 00000000300C: 8205FF05 00000000
+\ts_setpc_b64 s[4:5]                                         // 000000003014: BE801D04
+\ts_setpc_b64 s[30:31]                                       // 000000003018: BE801D1E
+"""
+
+
+def test_isa_check_detects_the_hung_shape():
+    bad = isa_check.find_hazards_in_listing(HUNG_SHAPE)
+    assert [b[0] for b in bad] == ["_ZN3hbx15cyc_exp_abs_x_dE"]  # kernels and other pairs are fine
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built")
+def test_library_has_no_far_branch_through_return_address():
+    assert isa_check.find_hazards(LIB) == []
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built")
+def test_dpp_guards_are_compiled_in():
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as tmp:
+        traps = 0
+        for co in isa_check._code_objects(LIB, tmp):
+            dis = subprocess.run([f"{isa_check.LLVM}/llvm-objdump", "-d", f"--mcpu={isa_check.ARCH}", co],
+                                 capture_output=True, text=True, check=True).stdout
+            traps += dis.count("s_trap 2")
+    assert traps > 0

@@ -1,0 +1,106 @@
+"""Static check of the gfx950 code objects in libhbx.so (or an object file) for the hazard that hung
+three earlier builds (DESIGN.md §4.2 "The hang").
+
+Mechanism, found in the disassembly of the hung coin build (commit 22714e6, cyc_exp_abs_x_d): a
+non-kernel function returns with ``s_setpc_b64 s[30:31]`` (the return address of the AMDGPU
+calling convention).  When such a function's body is larger than the +-128 KiB reach of
+``s_cbranch``/``s_branch``, LLVM's branch relaxation rewrites far branches as
+``s_getpc_b64 sX; s_add_u32; s_addc_u32; s_setpc_b64 sX`` -- and in a leaf function it used
+s[30:31] for sX without saving it.  The return then jumps to the last far-branch target inside the
+function's own loop: the wave never leaves the function (the printf trace of the r03e build
+entered the first exp-by-|x| and never returned).  Kernels are not affected (they end in
+s_endpgm; nothing lives in s[30:31]).
+
+``find_hazards`` lists every non-kernel function that performs a far branch through s[30:31]
+(an ``s_setpc_b64 s[30:31]`` that is preceded by an ``s_add_u32 s30`` of a relaxation sequence)
+and also returns through s[30:31].  tests/test_isa.py asserts the shipped library has none.
+
+Usage: python tools/isa_check.py [path.so|path.o ...]
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+ARCH = "gfx950"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _code_objects(path: str, tmp: str):
+    """Device code objects (ELF) inside a host .so/.o's .hip_fatbin section."""
+    fat = os.path.join(tmp, "fatbin")
+    subprocess.check_call([f"{LLVM}/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, path, os.path.join(tmp, "x")],
+                          stderr=subprocess.DEVNULL)
+    out = []
+    data = open(fat, "rb").read()
+    # a linked .so holds one bundle per translation unit: split at the bundle magic
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    for k, s in enumerate(starts):
+        e = starts[k + 1] if k + 1 < len(starts) else len(data)
+        b = os.path.join(tmp, f"b{k}")
+        open(b, "wb").write(data[s:e])
+        co = os.path.join(tmp, f"co{k}")
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o",
+                            f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}", f"--input={b}", f"--output={co}",
+                            "--unbundle"], stderr=subprocess.DEVNULL)
+        if r.returncode == 0 and os.path.getsize(co) > 0:
+            out.append(co)
+    return out
+
+
+def _functions(disasm: str):
+    """(name, [instruction lines]) per symbol of an llvm-objdump listing."""
+    name, body = None, []
+    for line in disasm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            if name:
+                yield name, body
+            name, body = m.group(1), []
+        elif name and line.startswith("\t"):
+            body.append(line.strip().split("//")[0].strip())
+    if name:
+        yield name, body
+
+
+def find_hazards_in_listing(disasm: str):
+    bad = []
+    for name, body in _functions(disasm):
+        if any(i.startswith("s_endpgm") for i in body):
+            continue  # a kernel
+        returns = any(i == "s_setpc_b64 s[30:31]" for i in body)
+        far = 0
+        for k, ins in enumerate(body):
+            if ins == "s_setpc_b64 s[30:31]" and k >= 1 and body[k - 1].startswith("s_addc_u32 s31"):
+                far += 1
+        if returns and far:
+            bad.append((name, far, len(body)))
+    return bad
+
+
+def find_hazards(path: str):
+    with tempfile.TemporaryDirectory() as tmp:
+        bad = []
+        for co in _code_objects(path, tmp):
+            dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", co], capture_output=True,
+                                 text=True, check=True).stdout
+            bad += find_hazards_in_listing(dis)
+        return bad
+
+
+if __name__ == "__main__":
+    paths = sys.argv[1:] or [os.path.join(ROOT, "hbbft_amd", "libhbx.so")]
+    rc = 0
+    for p in paths:
+        hz = find_hazards(p)
+        for name, far, n in hz:
+            print(f"{p}: {name}: {far} far branch(es) through the return address s[30:31] ({n} instructions)")
+            rc = 1
+        if not hz:
+            print(f"{p}: no far branch through s[30:31] in any returning function")
+    sys.exit(rc)
