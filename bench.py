@@ -74,7 +74,7 @@ HBM_PEAK_GBPS = 8000.0
 OWN_INDEX = 0  # the benchmarked node is validator 0 (own share computed locally, hbx_set_own_share)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--no-own-share", action="store_true",
                     help="run Ciphertext::verify as separate checks instead of through the node's own share")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per config")
-    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3, 6),
+    ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3, 6, 7),
                     help="lanes per decryption-share check (0: auto by occupancy)")
     ap.add_argument("--in-flight", type=int, default=2,
                     help="also time this many consecutive epochs in flight at once (one context and stream "
@@ -96,8 +96,13 @@ def parse():
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
     ap.add_argument("--configs", default="C2,C4,C5",
-                    help="secondary BASELINE configs in the same line (single GPU only; '' for none)")
-    return ap.parse_args()
+                    help="secondary BASELINE configs in the same line ('' for none); at --gpus > 1 (strong) C4 "
+                         "and C5 run sharded by instance")
+    return ap.parse_args(argv)
+
+
+def parse_args_for_test(argv):
+    return parse(argv)
 
 
 def host_info():
@@ -455,21 +460,36 @@ def config_c4(args, dev, torch, Context):
         bad[ii[0], ii[1]] = sigs[(ii[0] + 1) % inst, ii[1]]
         steps = max(args.steps, 3)
         wall = []
-        ctx.prepare_nonces(nonces)  # warm-up round
-        ctx.verify_sig_shares(bad)
-        ctx.combine_signatures(master_pk, t)
+        # the round on HBM-resident buffers (hbx_verify_sig_shares_d / hbx_combine_signatures_d):
+        # the shares are already on the device, as they would be after the transport's copy
+        d_bad = torch.from_numpy(bad).to(dev)
+        d_vst = torch.zeros((inst, n), dtype=torch.uint8, device=dev)
+        d_sig = torch.zeros((inst, 96), dtype=torch.uint8, device=dev)
+        d_st = torch.zeros(inst, dtype=torch.int32, device=dev)
+        d_ok = torch.zeros(inst, dtype=torch.uint8, device=dev)
+        d_par = torch.zeros(inst, dtype=torch.uint8, device=dev)
+
+        def round_():
+            ctx.prepare_nonces(nonces)
+            ctx.verify_sig_shares_d(d_bad, None, d_vst)
+            ctx.combine_signatures_d(master_pk, t, None, d_sig, d_st, d_ok, d_par)
+
+        round_()  # warm-up round
+        torch.cuda.synchronize(dev)
         ctx.set_timing(True)
         for _ in range(steps):
             t0 = time.perf_counter()
-            ctx.prepare_nonces(nonces)
-            valid = ctx.verify_sig_shares(bad)
-            sig, st, ok, par = ctx.combine_signatures(master_pk, t)
+            round_()
+            torch.cuda.synchronize(dev)
             wall.append(time.perf_counter() - t0)
         kern = {}
         for name in ("hash_nonces", "prepare_lines", "verify_sig", "combine_sigs"):
             ms_, cnt_ = ctx.kernel_time(name)
-            kern[name] = round(ms_ / max(cnt_, 1), 3)
+            kern[name] = round(ms_ / max(cnt_, 1), 3) if cnt_ else 0.0
         ctx.set_timing(False)
+        lanes = ctx.coin_lanes_used()
+        valid = d_vst.cpu().numpy() == 1
+        st, ok = d_st.cpu().numpy(), d_ok.cpu().numpy().astype(bool)
     assert (valid == ~corrupt).all(), "signature-share validity"
     assert (st == 0).all() and ok.all(), "combine / master verification"
     kms = kern["verify_sig"]
@@ -481,11 +501,13 @@ def config_c4(args, dev, torch, Context):
            "value": round(inst * n / (kms * 1e-3), 1), "unit": "sig-share verifies/s (verify kernel, HIP events)",
            "round_ms_kernels": round(round_kernels, 3),
            "round_ms_wall": round(1e3 * float(np.mean(wall)), 3),
-           "wall_note": "host API: the wall time includes PCIe staging of 3.1 MB of signature shares and readbacks",
-           "kernels_ms": kern,
+           "wall_note": "device API (hbx_verify_sig_shares_d / hbx_combine_signatures_d) on HBM-resident shares; "
+                        "hbx_prepare_nonces uploads the 256 nonces and synchronises",
+           "kernels_ms": kern, "coin_lanes": lanes,
            "roofline": {"bound": "valu-int (v_mad_u64_u32)", "achieved": round(achieved, 3), "peak": PEAK_TMAD_S,
                         "unit": "Tmad/s", "frac": round(achieved / PEAK_TMAD_S, 4), "traffic": None,
-                        "kernel": "k_verify_sig_shares2 (two lanes per check: 512 one-lane waves would fill half the chip)",
+                        "kernel": ("k_verify_sig_shares2 (two lanes per check: 512 one-lane waves would fill half the chip)"
+                                   if lanes == 2 else "k_verify_sig_shares (one lane per check)"),
                         "kernel_ms": kms,
                         "work": f"{inst * n} checks x {VSIG_FQMUL} Fq-mul (frozen unit V_sig) x {MADS_PER_FQMUL} MAD",
                         "opcount": {"fqmul_per_check": OPCOUNT_VSIG, "frac": round(achieved_op / PEAK_TMAD_S, 4)}}}
@@ -796,6 +818,127 @@ def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
 
 
 # ----------------------------------------------------------------------------------------------
+# Stacks B and C across GPUs: instance sharding + one all-gather of result slabs
+# ----------------------------------------------------------------------------------------------
+def _timed_steps(torch, dist, dev, world, steps, fn):
+    """Barrier + synchronize on both sides of ``steps`` calls of fn; max over ranks (seconds)."""
+    fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def sharded_c4(args, dev, torch, Context, world, rank):
+    """C4 across ``world`` GPUs: rank g owns instances instance_range(256, world, g) -- their nonces,
+    the 128 signature shares of each, the combines; one all-gather of (share status, signature,
+    combine status, master-ok, parity) slabs gives every rank the round's result."""
+    import torch.distributed as dist
+
+    from hbbft_amd import netinfo, shard
+
+    n, inst = 128, 256
+    lo, hi = shard.instance_range(inst, world, rank)
+    c = hi - lo
+    lay = shard.coin_layout(inst, n, world)
+    with Context(dev.index or 0) as ctx:
+        sks, sk_shares, master_sk = netinfo.generate_keys(n)
+        t = sks.threshold + 1
+        pk = ctx.public_keys(sk_shares)
+        master_pk = ctx.public_keys(master_sk)[0].tobytes()
+        assert (ctx.set_pk_shares([r.tobytes() for r in pk]) == 0).all()
+        inv_id = "[" + ", ".join(str(b) for b in master_pk) + "]"
+        nonces = [f"Nonce for Honey Badger {inv_id}@{s}:2:{j}".encode() for s in (0, 1) for j in range(n)][lo:hi]
+        ctx.prepare_nonces(nonces)
+        sigs = ctx.sign(sk_shares)
+        corrupt = (np.random.default_rng(0x68626278_00000005).integers(0, 64, size=(inst, n)) == 0)
+        bad = sigs.copy()
+        ii = np.nonzero(corrupt[lo:hi])
+        bad[ii[0], ii[1]] = sigs[(ii[0] + 1) % c, ii[1]]  # another instance's share of the same signer
+        expect = corrupt  # every rank substitutes within its own slice (c > 1 at 256 instances)
+        slab = torch.zeros(lay.size, dtype=torch.uint8, device=dev)
+        d_bad = torch.from_numpy(bad).to(dev)
+        v = {name: lay.view(slab, name, c) for name in lay.fields}
+        gathered = [None]
+
+        def step():
+            ctx.prepare_nonces(nonces)
+            ctx.verify_sig_shares_d(d_bad, None, v["share_status"])
+            ctx.combine_signatures_d(master_pk, t, None, v["sig"], v["comb_status"], v["master_ok"], v["parity"])
+            gathered[0] = shard.all_gather_slabs(slab, world)
+
+        steps = max(args.steps, 3)
+        el = _timed_steps(torch, dist, dev, world, steps, step)
+        full = shard.assemble_fields(gathered[0].cpu().numpy(), lay, inst, world)
+    assert ((full["share_status"] == 1) == ~expect).all(), "gathered signature-share statuses"
+    assert (full["comb_status"] == 0).all() and (full["master_ok"] == 1).all(), "gathered combines"
+    return {"workload": f"CommonCoin N={n} x {inst} instances sharded by instance over {world} GPUs "
+                        f"(+ one all-gather of {lay.size} B result slabs)",
+            "value": round(inst * n * steps / el, 1), "unit": "sig-share verifies/s (whole job, wall)",
+            "ms_per_round": round(el / steps * 1e3, 3), "instances_per_gpu": c, "scaling": "strong"}
+
+
+def sharded_c5(args, dev, torch, Context, world, rank):
+    """C5 across ``world`` GPUs: rank g owns proposals instance_range(128, world, g): encode, SHA-256
+    Merkle roots and the decode with the last 42 shards missing; one all-gather of (root, decode
+    status, output length) slabs; payloads stay on the owning GPU."""
+    import torch.distributed as dist
+
+    from hbbft_amd import shard
+
+    n, f = 128, 42
+    k, m = n - 2 * f, 2 * f
+    inst, plen = 128, 1 << 20
+    L = (plen + 4 + k - 1) // k
+    lo, hi = shard.instance_range(inst, world, rank)
+    c = hi - lo
+    rng = np.random.default_rng(0x68626278_00000006)
+    payload = rng.integers(0, 256, size=(inst, plen), dtype=np.uint8)[lo:hi]
+    frame = np.zeros((c, k * L), dtype=np.uint8)
+    frame[:, :4] = np.frombuffer(np.uint32(plen).byteswap().tobytes(), dtype=np.uint8)
+    frame[:, 4:4 + plen] = payload
+    host = np.zeros((c, n, L), dtype=np.uint8)
+    host[:, :k] = frame.reshape(c, k, L)
+    shards = torch.from_numpy(host).to(dev)
+    present = torch.ones((c, n), dtype=torch.uint8, device=dev)
+    present[:, n - f:] = 0
+    out = torch.zeros((c, k * L), dtype=torch.uint8, device=dev)
+    work = torch.empty_like(shards)
+    lay = shard.broadcast_layout(inst, world)
+    slab = torch.zeros(lay.size, dtype=torch.uint8, device=dev)
+    v = {name: lay.view(slab, name, c) for name in lay.fields}
+    gathered = [None]
+    with Context(dev.index or 0) as ctx:
+        ctx.set_merkle_digest(0)
+
+        def step():
+            ctx.rs_encode_d(shards, k, m)
+            ctx.merkle_roots_d(shards, v["root"])
+            work.copy_(shards)
+            work[:, n - f:] = 0xA5
+            ctx.broadcast_decode_d(work, present, v["root"], k, m, out, v["out_len"], v["decode_status"])
+            gathered[0] = shard.all_gather_slabs(slab, world)
+
+        steps = max(args.steps, 3)
+        el = _timed_steps(torch, dist, dev, world, steps, step)
+        full = shard.assemble_fields(gathered[0].cpu().numpy(), lay, inst, world)
+        assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "decoded payload"
+    assert (full["decode_status"] == 0).all() and (full["out_len"] == plen).all(), "gathered decodes"
+    return {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} 1 MiB proposals sharded by instance over {world} "
+                        f"GPUs (encode + SHA-256 roots + decode, + one all-gather of {lay.size} B slabs)",
+            "value": round(inst * plen * steps / el / 1e9, 2), "unit": "GB/s of proposals (whole job, wall)",
+            "ms_per_round": round(el / steps * 1e3, 3), "instances_per_gpu": c, "scaling": "strong"}
+
+
+# ----------------------------------------------------------------------------------------------
 def main():
     args = parse()
     import torch
@@ -920,6 +1063,13 @@ def main():
             if fn is None:
                 raise SystemExit(f"unknown config {name}")
             cfgs[name] = fn(args, dev, torch, Context)
+        res["configs"] = cfgs
+    if world > 1 and strong and args.configs:
+        cfgs = {}
+        for name in [c.strip().upper() for c in args.configs.split(",") if c.strip()]:
+            fn = {"C4": sharded_c4, "C5": sharded_c5}.get(name)
+            if fn is not None:  # C2 is a single-GPU config (BASELINE: "on 1 MI355X")
+                cfgs[name] = fn(args, dev, torch, Context, world, rank)
         res["configs"] = cfgs
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -1,0 +1,424 @@
+// The one-lane share check's final exponentiation as a chain of STEP kernels (k_fe1<STEP>), in the
+// signed-digit tower (fieldd.hpp).  Same element as pairingd.hpp final_exponentiation_d (and
+// pairing.hpp final_exponentiation): f^(3 (p^12 - 1)/r), compared with 1 -- the verdict of
+// PublicKeyShare::verify_decryption_share (honey_badger.rs:229 via threshold_crypto; SURVEY.md
+// §8(a) rows A1, A9).
+//
+// Why a chain of kernels.  Inside one kernel the exponentiation's Fq12 values crossed out-of-line
+// calls through the lane's scratch stack: 8.7 KB/lane of frames, 18.7 GB of scratch traffic per
+// N=256 launch and ~20 % of the wave's cycles waiting on it.  Here nothing leaves
+// the registers inside a kernel except through explicit slots:
+//   * the running value r (one Fq12, 168 registers) stays in registers for a whole step;
+//   * the exponentiation base / product operand sits in the lane's LDS slot A (one packed Fq12,
+//     156 dwords, lane-interleaved: one wave per SIMD fills a CU's 160 KB), streamed one Fq2
+//     coefficient at a time into the products (fq12d_mul_slot), so a product holds r, three Fq6
+//     accumulators and one Fq2 product's temporaries;
+//   * the values that live across exponentiations (t^3 then d, a, b) go to coalesced global slots
+//     between kernels: 3 packed Fq12 per check, [wave][slot][word][64 lanes] (~7.5 KB of traffic
+//     per check in total instead of ~285 KB of frames).
+// Every step is one kernel, so the register allocator sees at most one exponentiation loop and
+// two products at a time, and there are no call frames at all.
+//
+// Chain (pairing.hpp final_exponentiation, regrouped as pairing2d.hpp FE2_PROG), one kernel each:
+//   F0  t0 = conj(f)^2 / N(f) (= conj(f) f^-1, N(f) = f0^2 - v f1^2 in Fq6: one Fq6 inverse);
+//       t = frob2(t0) t0                                                      -> slot G
+//   F1  a = conj(t^|x| t); t^3 is the value after the first run of t^|x|      -> slot G, T
+//   F2  a = conj(a^|x| a)                                                      -> slot G
+//   F3  b = conj(a^|x|) frob(a)                                                -> slot F
+//   F4  d = t^3 conj(b) frob2(b)                                               -> slot T
+//   F5  u = b^|x|                                                              -> slot G
+//   F6  u^|x| d == 1  (= b^(x^2) d = f^(3 (p^12 - 1)/r))
+#pragma once
+#include "pairingd.hpp"
+
+namespace hbx {
+
+// ---- one-lane slots: a packed Fq12 (12 Fq x 13 dwords, pairingd.hpp lds_put_fq12d's packing),
+// word k of this lane at p[k * S] ------------------------------------------------------------------
+constexpr int FE1_WORDS = 156;
+template <int S, class P>
+HBX_HD fqd s1_get_fqd(P p, int word) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) w[k] = p[(word + k) * S];
+  fqd e;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    uint32_t d = w[wd] >> sh;
+    if (sh > 4) d |= w[wd + 1] << (32 - sh);
+    e.d[i] = (int32_t)(d & (uint32_t)DMASK);
+    HBX_LAUNDER(e.d[i]);
+  }
+  e.d[13] = (int32_t)w[12];
+  return e;
+}
+// e normalised: digits 0..12 in [0, 2^28), digit 13 whole
+template <int S, class P>
+HBX_HD void s1_put_fqd(P p, int word, const fqd& e) {
+  uint32_t w[13];
+#pragma unroll
+  for (int k = 0; k < 12; k++) w[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) {
+    const int off = 28 * i, wd = off >> 5, sh = off & 31;
+    const uint32_t d = (uint32_t)e.d[i];
+    w[wd] |= d << sh;
+    if (sh > 4) w[wd + 1] |= d >> (32 - sh);
+  }
+  w[12] = (uint32_t)e.d[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) p[(word + k) * S] = w[k];
+}
+// Fq2 coefficient q (0..5: c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2)
+template <int S, class P>
+HBX_HD fq2d s1_get_fq2d(P p, int q) {
+  return fq2d{s1_get_fqd<S>(p, 26 * q), s1_get_fqd<S>(p, 26 * q + 13)};
+}
+template <int S, class P>
+HBX_HD void s1_put_fq2d(P p, int q, const fq2d& a) {
+  s1_put_fqd<S>(p, 26 * q, a.c0);
+  s1_put_fqd<S>(p, 26 * q + 13, a.c1);
+}
+// Whole-Fq12 loads / stores go one Fq2 coefficient at a time behind fences: unfenced, the
+// scheduler issues all 156 loads (or packs all 12 elements) at once, and those temporaries beside
+// a live Fq12 are what made the steps spill.
+template <int S, class P>
+HBX_HD fq12d s1_get_fq12d(P p) {
+  const fq2d c0 = s1_get_fq2d<S>(p, 0);
+  HBX_SEQ();
+  const fq2d c1 = s1_get_fq2d<S>(p, 1);
+  HBX_SEQ();
+  const fq2d c2 = s1_get_fq2d<S>(p, 2);
+  HBX_SEQ();
+  const fq2d c3 = s1_get_fq2d<S>(p, 3);
+  HBX_SEQ();
+  const fq2d c4 = s1_get_fq2d<S>(p, 4);
+  HBX_SEQ();
+  const fq2d c5 = s1_get_fq2d<S>(p, 5);
+  HBX_SEQ();
+  return fq12d{fq6d{c0, c1, c2}, fq6d{c3, c4, c5}};
+}
+template <int S, class P>
+HBX_HD void s1_put_fq12d(P p, const fq12d& a) {
+  s1_put_fq2d<S>(p, 0, a.c0.c0);
+  HBX_SEQ();
+  s1_put_fq2d<S>(p, 1, a.c0.c1);
+  HBX_SEQ();
+  s1_put_fq2d<S>(p, 2, a.c0.c2);
+  HBX_SEQ();
+  s1_put_fq2d<S>(p, 3, a.c1.c0);
+  HBX_SEQ();
+  s1_put_fq2d<S>(p, 4, a.c1.c1);
+  HBX_SEQ();
+  s1_put_fq2d<S>(p, 5, a.c1.c2);
+  HBX_SEQ();
+}
+// slot-to-slot copy (global -> LDS), 52 words (two Fq2 coefficients) in flight at a time
+template <int SD, int SS, class PD, class PS>
+HBX_HD void s1_copy(PD d, PS s) {
+#pragma unroll 1
+  for (int k0 = 0; k0 < FE1_WORDS; k0 += 52) {
+#pragma unroll
+    for (int k = 0; k < 52; k++) d[(k0 + k) * SD] = s[(k0 + k) * SS];
+    HBX_SEQ();
+  }
+}
+
+HBX_HD fq6d fq6d_zero_() {
+  const fqd z = fqd_zero();
+  return fq6d{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
+}
+
+// acc += a * y (fieldd.hpp fq6d_mul's Karatsuba), y(q) its Fq2 coefficient q, every Fq2 product
+// folded into the accumulator at once, a fence between products (HBX_SEQ); a and y normalised,
+// acc normalised (or zero) on entry; carry-normalised on exit.  The digit sums stay below 2^31:
+// acc + 7 terms of at most two normalised values each.
+template <class Y>
+HBX_HD void fq6d_mul_acc1(fq6d& acc, const fq6d& a, Y y) {
+  {
+    const fq2d t0 = fq2d_mul(a.c0, y(0));
+    acc.c0 = fq2d_add(acc.c0, t0);
+    acc.c1 = fq2d_sub(acc.c1, t0);
+    acc.c2 = fq2d_sub(acc.c2, t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(a.c1, y(1));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
+    acc.c1 = fq2d_sub(acc.c1, t1);
+    acc.c2 = fq2d_add(acc.c2, t1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t2 = fq2d_mul(a.c2, y(2));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
+    acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
+    acc.c2 = fq2d_sub(acc.c2, t2);
+  }
+  HBX_SEQ();
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))));
+  HBX_SEQ();
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))));
+  HBX_SEQ();
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))));
+  HBX_SEQ();
+  acc = fq6d_norm(acc);
+}
+
+// X * Y, X in registers (reduced, or its conjugate), Y the packed value in slot y.  Reduced.
+// Karatsuba over w: c0 = X0 Y0 + v X1 Y1, c1 = (X0 + X1)(Y0 + Y1) - X0 Y0 - X1 Y1.
+template <int S, class P>
+HBX_HD fq12d fq12d_mul_slot(const fq12d& X, P y) {
+  fq6d A = fq6d_zero_();
+  fq6d_mul_acc1(A, X.c0, [&](int q) { return s1_get_fq2d<S>(y, q); });
+  HBX_SEQ();
+  fq6d B = fq6d_zero_();
+  fq6d_mul_acc1(B, X.c1, [&](int q) { return s1_get_fq2d<S>(y, 3 + q); });
+  HBX_SEQ();
+  fq6d C = fq6d_zero_();
+  const fq6d Xs = fq6d_norm(fq6d_add(X.c0, X.c1));
+  fq6d_mul_acc1(C, Xs, [&](int q) { return fq2d_norm(fq2d_add(s1_get_fq2d<S>(y, q), s1_get_fq2d<S>(y, 3 + q))); });
+  return fq12d{fq6d_reduce(fq6d_add(A, fq6d_mul_v(B))), fq6d_reduce(fq6d_sub(fq6d_sub(C, A), B))};
+}
+
+// Granger-Scott cyclotomic squaring (fieldd.hpp fq12d_cyclotomic_sqr) with a fence after every Fq2
+// squaring: the nine squarings are independent, and unfenced the scheduler interleaves them until
+// the temporaries of all of them are live at once (440 VGPRs spilled around a bare loop of them).
+#ifndef HBX_FE1_CYC_FENCE
+#define HBX_FE1_CYC_FENCE 2  // 2: after every Fq2 squaring, 1: after every Fq4 squaring, 0: none
+#endif
+#if HBX_FE1_CYC_FENCE >= 2
+#define HBX_CYC_SEQ2() HBX_SEQ()
+#else
+#define HBX_CYC_SEQ2() ((void)0)
+#endif
+#if HBX_FE1_CYC_FENCE >= 1
+#define HBX_CYC_SEQ1() HBX_SEQ()
+#else
+#define HBX_CYC_SEQ1() ((void)0)
+#endif
+HBX_HD void fq4d_sqr_seq(const fq2d& a, const fq2d& b, fq2d& c0, fq2d& c1) {
+  const fq2d t0 = fq2d_sqr(a);
+  HBX_CYC_SEQ2();
+  const fq2d t1 = fq2d_sqr(b);
+  HBX_CYC_SEQ2();
+  c0 = fq2d_norm(fq2d_add(fq2d_mul_xi(t1), t0));
+  c1 = fq2d_norm(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(a, b)), t0), t1));
+  HBX_CYC_SEQ1();
+}
+HBX_HD fq12d fq12d_cyclotomic_sqr_seq(const fq12d& f) {
+  fq2d z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
+  fq2d z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fq2d t0, t1;
+  fq4d_sqr_seq(z0, z1, t0, t1);
+  z0 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t0, z0)), t0));
+  z1 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t1, z1)), t1));
+  fq4d_sqr_seq(z4, z5, t0, t1);  // (z4, z5) before they are replaced: t2, t3 of fieldd.hpp
+  const fq2d n3 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t0, z3)), t0));
+  t0 = fq2d_mul_xi(t1);
+  const fq2d n2 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t0, z2)), t0));
+  fq4d_sqr_seq(z2, z3, t0, t1);
+  z4 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_sub(t0, z4)), t0));
+  z5 = fq2d_reduce(fq2d_add(fq2d_dbl(fq2d_add(t1, z5)), t1));
+  return fq12d{fq6d{z0, z4, n3}, fq6d{n2, z1, z5}};
+}
+
+// r^|x| with r's value also in slot a (the base): squaring runs between the one bits of |x| (63,
+// 62, 60, 57, 48, 16), a product by the base after each run but the last.  If t3 is given, the
+// value after the first run and product (r^3) is stored there.
+template <int S, int SG, class P, class PG>
+HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3) {
+  static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
+#pragma unroll 1
+  for (int q = 0; q < 6; q++) {
+    const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
+#pragma unroll 1
+    for (int i = 0; i < run; i++) r = fq12d_cyclotomic_sqr_seq(r);
+    if (q < 5) {
+      HBX_SEQ();
+      r = fq12d_mul_slot<S>(r, a);
+      if (q == 0 && t3) s1_put_fq12d<SG>(t3, r);
+    }
+  }
+  return r;
+}
+
+// slot a <- map(slot a) in place, one Fq2 coefficient at a time: MAP 1 = f^p, 2 = f^(p^2)
+// (fieldd.hpp fq12d_frobenius / fq12d_frobenius2: coefficient c_h.c_k is gamma index 2k + h)
+template <int S, int MAP, class P>
+HBX_HD void s1_frob_inplace(P a) {
+#pragma unroll 1
+  for (int q = 0; q < 6; q++) {
+    const int i = 2 * (q % 3) + q / 3;
+    fq2d y = s1_get_fq2d<S>(a, q);
+    if (MAP == 1) {
+      y = fq2d_conj(y);
+      if (i) {
+        const int32_t* k0 = i == 1 ? FROBD1_C1_0 : i == 2 ? FROBD1_C2_0 : i == 3 ? FROBD1_C3_0 : i == 4 ? FROBD1_C4_0 : FROBD1_C5_0;
+        const int32_t* k1 = i == 1 ? FROBD1_C1_1 : i == 2 ? FROBD1_C2_1 : i == 3 ? FROBD1_C3_1 : i == 4 ? FROBD1_C4_1 : FROBD1_C5_1;
+        y = fq2d_mul(y, fq2d_const(k0, k1));
+      } else {
+        y = fq2d_norm(y);
+      }
+    } else if (i) {
+      const int32_t* kk = i == 1 ? FROBD2_C1 : i == 2 ? FROBD2_C2 : i == 3 ? FROBD2_C3 : i == 4 ? FROBD2_C4 : FROBD2_C5;
+      y = fq2d_mul_fq(y, fqd_const(kk));
+    }
+    s1_put_fq2d<S>(a, q, y);
+  }
+}
+
+// ---- STEP 0 pieces ---------------------------------------------------------------------------
+// Fq6 inverse of a (reduced) into slot words [0, 78) of y (fieldd.hpp tower; one Fq inversion):
+// c0 = a0^2 - xi a1 a2, c1 = xi a2^2 - a0 a1, c2 = a1^2 - a0 a2, t = a0 c0 + xi (a2 c1 + a1 c2),
+// a^-1 = (c0, c1, c2) conj(t) / (t0^2 + t1^2).  The packed coefficients are normalised.
+template <int S, class P>
+HBX_HD void fq6d_inv_to_slot(const fq6d& a, P y) {
+  fq2d t;
+  {
+    const fq2d c0 = fq2d_reduce(fq2d_sub(fq2d_sqr(a.c0), fq2d_mul_xi(fq2d_mul(a.c1, a.c2))));
+    s1_put_fq2d<S>(y, 0, c0);
+    t = fq2d_mul(a.c0, c0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d c1 = fq2d_reduce(fq2d_sub(fq2d_mul_xi(fq2d_sqr(a.c2)), fq2d_mul(a.c0, a.c1)));
+    s1_put_fq2d<S>(y, 1, c1);
+    t = fq2d_add(t, fq2d_mul_xi(fq2d_mul(a.c2, c1)));
+  }
+  HBX_SEQ();
+  {
+    const fq2d c2 = fq2d_reduce(fq2d_sub(fq2d_sqr(a.c1), fq2d_mul(a.c0, a.c2)));
+    s1_put_fq2d<S>(y, 2, c2);
+    t = fq2d_reduce(fq2d_add(t, fq2d_mul_xi(fq2d_mul(a.c1, c2))));
+  }
+  HBX_SEQ();
+  const fqd nrm = fqd_reduce(fqd_add(fqd_sqr(t.c0), fqd_sqr(t.c1)));
+  HBX_SEQ();
+  const fqd ni = fqd_from_fq(fq_inv_i(fqd_to_fq(nrm)));
+  HBX_SEQ();
+  const fq2d ti = fq2d_mul_fq(fq2d_conj(t), ni);
+#pragma unroll 1
+  for (int q = 0; q < 3; q++) {
+    HBX_SEQ();
+    s1_put_fq2d<S>(y, q, fq2d_reduce(fq2d_mul(s1_get_fq2d<S>(y, q), ti)));
+  }
+}
+
+// t0 = conj(f) / f = conj(f)^2 / N(f) with N(f) = f0^2 - v f1^2 (f reduced, f != 0); slot a is
+// scratch.  Reduced.
+template <int S, class P>
+HBX_HD fq12d fe1_easy_first(const fq12d& f, P a) {
+  {
+    const fq6d n = fq6d_reduce(fq6d_sub(fq6d_mul(f.c0, f.c0), fq6d_mul_v(fq6d_mul(f.c1, f.c1))));
+    HBX_SEQ();
+    fq6d_inv_to_slot<S>(n, a);  // words [0, 78): N^-1
+  }
+  HBX_SEQ();
+  const fq12d g = fq12d_sqr(fq12d_conj(f));
+  HBX_SEQ();
+  fq6d A = fq6d_zero_(), B = fq6d_zero_();
+  fq6d_mul_acc1(A, g.c0, [&](int q) { return s1_get_fq2d<S>(a, q); });
+  HBX_SEQ();
+  fq6d_mul_acc1(B, g.c1, [&](int q) { return s1_get_fq2d<S>(a, q); });
+  return fq12d{fq6d_reduce(A), fq6d_reduce(B)};
+}
+
+// fq12d_is_one with the conversions one Fq at a time (no Fq12 in a call frame)
+HBX_HD bool fq12d_is_one_seq(const fq12d& a) {
+  const fqd* e = &a.c0.c0.c0;
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < 12; q++) {
+    const fq v = fq_canon(fqd_to_fq(e[q]));
+    ok = ok && (q == 0 ? fq_eq(v, fq_one()) : fq_is_zero(v));
+  }
+  return ok;
+}
+
+// ---- the seven steps over a lane's slots: a = LDS (or host) slot, gf / gt / gg = global slots F
+// (Miller output, later b), T (t^3, later d), G (t, a, u) ------------------------------------------
+constexpr int FE1_STEPS = 7;
+// F0: t = frob2(t0) t0, t0 = conj(f) / f  -> G
+template <int S, int SG, class P, class PG>
+HBX_HD void fe1_step0(P a, PG gf, PG gg) {
+  fq12d r = fe1_easy_first<S>(s1_get_fq12d<SG>(gf), a);  // t0
+  HBX_SEQ();
+  s1_put_fq12d<S>(a, r);
+  HBX_SEQ();
+  r = fq12d_mul_slot<S>(fq12d_frobenius2(r), a);
+  s1_put_fq12d<SG>(gg, r);
+}
+// F1, F2: x -> conj(x^|x| x) (x = t: t^3 -> T on the way; then x = a)
+template <int S, int SG, class P, class PG>
+HBX_HD void fe1_step_expmul(P a, PG gt, PG gg) {
+  s1_copy<S, SG>(a, gg);
+  HBX_SEQ();
+  fq12d r = s1_get_fq12d<S>(a);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, gt);
+  HBX_SEQ();
+  r = fq12d_mul_slot<S>(r, a);
+  s1_put_fq12d<SG>(gg, fq12d{r.c0, fq6d_norm(fq6d_neg(r.c1))});
+}
+// F3: b = conj(a^|x|) frob(a)  -> F
+template <int S, int SG, class P, class PG>
+HBX_HD void fe1_step3(P a, PG gf, PG gg) {
+  s1_copy<S, SG>(a, gg);
+  HBX_SEQ();
+  fq12d r = s1_get_fq12d<S>(a);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  HBX_SEQ();
+  s1_frob_inplace<S, 1>(a);
+  HBX_SEQ();
+  r = fq12d_mul_slot<S>(fq12d_conj(r), a);
+  s1_put_fq12d<SG>(gf, r);
+}
+// F4: d = t^3 conj(b) frob2(b)  -> T
+template <int S, int SG, class P, class PG>
+HBX_HD void fe1_step4(P a, PG gf, PG gt) {
+  s1_copy<S, SG>(a, gf);
+  HBX_SEQ();
+  s1_frob_inplace<S, 2>(a);
+  HBX_SEQ();
+  fq12d r = fq12d_mul_slot<S>(fq12d_conj(s1_get_fq12d<SG>(gf)), a);
+  HBX_SEQ();
+  s1_copy<S, SG>(a, gt);
+  HBX_SEQ();
+  r = fq12d_mul_slot<S>(r, a);
+  s1_put_fq12d<SG>(gt, r);
+}
+// F5: u = b^|x|  -> G
+template <int S, int SG, class P, class PG>
+HBX_HD void fe1_step5(P a, PG gf, PG gg) {
+  s1_copy<S, SG>(a, gf);
+  HBX_SEQ();
+  fq12d r = s1_get_fq12d<S>(a);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  s1_put_fq12d<SG>(gg, r);
+}
+// F6: u^|x| d (= b^(x^2) d = f^(3 (p^12 - 1)/r)): == 1 iff the check holds
+template <int S, int SG, class P, class PG>
+HBX_HD fq12d fe1_step6(P a, PG gt, PG gg) {
+  s1_copy<S, SG>(a, gg);
+  HBX_SEQ();
+  fq12d r = s1_get_fq12d<S>(a);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  HBX_SEQ();
+  s1_copy<S, SG>(a, gt);
+  HBX_SEQ();
+  return fq12d_mul_slot<S>(r, a);
+}
+// the whole chain on one lane (host checks; the kernels run one step each)
+template <int S, int SG, class P, class PG>
+HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg) {
+  fe1_step0<S, SG>(a, gf, gg);
+  fe1_step_expmul<S, SG>(a, gt, gg);
+  fe1_step_expmul<S, SG>(a, (PG) nullptr, gg);
+  fe1_step3<S, SG>(a, gf, gg);
+  fe1_step4<S, SG>(a, gf, gt);
+  fe1_step5<S, SG>(a, gf, gg);
+  return fe1_step6<S, SG>(a, gt, gg);
+}
+
+}  // namespace hbx

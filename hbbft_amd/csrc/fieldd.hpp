@@ -59,6 +59,22 @@ namespace hbx {
 #define HBX_SEQ() ((void)0)
 #endif
 
+// Digit laundering.  `(int64_t)a * (int64_t)b` of two sign-extended digits is ONE v_mad_i64_i32 --
+// unless the compiler has proved one operand non-negative (a digit masked to 28 bits by a
+// normalisation, a reduction, a product or an unpacking): it then turns that sign extension into a
+// zero extension and expands the mixed-sign product into v_mad_u64_u32 plus a correction
+// multiply-add by the other operand's sign word and register moves (a cyclotomic squaring in the
+// final exponentiation steps measured 8,979 multiply-adds and 3,622 v_mov_b32 instead of ~7,100 and
+// ~0).  Every place that masks a digit passes it through an empty asm with the digit as an in/out
+// VGPR operand, which hides what is known about its value and emits nothing.  (Laundering the
+// product operands instead forced the Miller loop's wave-uniform line coefficients out of SGPRs
+// into VGPRs: more registers, spills.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HBX_LAUNDER(x) __asm__("" : "+v"(x))
+#else
+#define HBX_LAUNDER(x) ((void)0)
+#endif
+
 struct fqd {
   int32_t d[14];
 };
@@ -115,6 +131,7 @@ HBX_HD fqd fqd_norm(const fqd& a) {
     const int32_t v = a.d[i] + c;
     r.d[i] = v & DMASK;
     c = v >> 28;  // arithmetic: floor division
+    HBX_LAUNDER(r.d[i]);
   }
   r.d[13] = a.d[13] + c;
   return r;
@@ -132,6 +149,7 @@ HBX_HD fqd fqd_reduce(const fqd& a) {
     acc += (int64_t)a.d[i] - (int64_t)q * (int64_t)FQ_P28[i];
     r.d[i] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
     acc >>= 28;
+    HBX_LAUNDER(r.d[i]);
   }
   r.d[13] = (int32_t)(acc + (int64_t)a.d[13] - (int64_t)q * (int64_t)FQ_P28[13]);
   return r;
@@ -173,6 +191,7 @@ HBX_HD fqd fqd_mul(const fqd& a, const fqd& b) {
     } else {
       r.d[k - 14] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
       acc >>= 28;
+      HBX_LAUNDER(r.d[k - 14]);
     }
   }
   r.d[13] = (int32_t)acc;
@@ -216,11 +235,22 @@ HBX_HD fqd fqd_sqr(const fqd& a) {
     } else {
       r.d[k - 14] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
       acc >>= 28;
+      HBX_LAUNDER(r.d[k - 14]);
     }
   }
   r.d[13] = (int32_t)acc;
   return r;
 }
+
+// HBX_REDC_FENCE (set per translation unit): a scheduling barrier after every column of the fused
+// Fq2 product loops, so the scheduler cannot hoist later columns' multiply-adds -- at one wave per
+// SIMD it otherwise fills ~190 VGPRs with a single Fq2 product's partial sums, which leaves no
+// room for a live Fq12 (fe1d.hpp).
+#if defined(HBX_REDC_FENCE) && defined(__HIP_DEVICE_COMPILE__)
+#define HBX_COL_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define HBX_COL_FENCE() ((void)0)
+#endif
 
 // Two Montgomery reductions driven by one column loop: (x, y) with x = sum_k X_k 2^(28k),
 // y = sum_k Y_k 2^(28k) given column by column by `col` (X_k, Y_k exact in int64), returns
@@ -260,7 +290,10 @@ HBX_HD void fqd_redc2(Col col, fqd& rx, fqd& ry) {
       ry.d[k - 14] = (int32_t)((uint32_t)ay & (uint32_t)DMASK);
       ax >>= 28;
       ay >>= 28;
+      HBX_LAUNDER(rx.d[k - 14]);
+      HBX_LAUNDER(ry.d[k - 14]);
     }
+    HBX_COL_FENCE();
   }
   rx.d[13] = (int32_t)ax;
   ry.d[13] = (int32_t)ay;

@@ -87,6 +87,7 @@ struct hbx_ctx {
   // (0 = none: a prepare invalidates S / valid for the combine)
   uint32_t n_shares = 0, verified_p = 0;
   dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
+  dbuf fe1slot;  // one-lane checks: the final exponentiation's global slots F, T, G (fe1d.hpp)
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -100,6 +101,10 @@ struct hbx_ctx {
   // PublicKey::verify batches (hbx_verify_sigs)
   dbuf vs_pk, vs_blob, vs_off, vs_H, vs_lines, vs_lines_d, vs_scratch, vs_sig96, vs_sig, vs_sig_st, vs_status;
   dbuf coin_lines_d;  // the nonces' lines in the coin check's digit form
+  bool coin_lines_ready = false;  // coin_lines_d computed for the prepared nonces (one-lane checks only)
+  uint8_t coin_mpk48[48] = {0};   // the master key coin_mpk was decoded from
+  bool coin_mpk_known = false;
+  dbuf coin_use;      // hbx_combine_signatures_d: the verified shares masked by the caller's subset
   // SyncKeyGen commitment checks (hbx_bivar_rows / hbx_bivar_check_acks)
   dbuf bv_commit48, bv_C, bv_cst, bv_rows, bv_rows48, bv_pst, bv_ackp, bv_acky, bv_vals, bv_out;
   // opt-in kernel timing: event pairs per timed kernel (hbx_set_timing / hbx_kernel_time)
@@ -479,7 +484,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
                   &c->vs_pk, &c->vs_lines_d, &c->coin_lines_d, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
-                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
+                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->fe1slot, &c->coin_use, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipEventDestroy(c->ev_last);
@@ -505,8 +510,8 @@ int hbx_set_digest(hbx_ctx* c, int variant) {
 }
 
 int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
-  if (!c || lanes < 0 || lanes > 6 || lanes == 4 || lanes == 5)
-    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1, 2, 3 or 6, not %d", lanes);
+  if (!c || lanes < 0 || lanes > 7 || lanes == 4 || lanes == 5)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_set_verify_lanes: 0 (auto), 1, 2, 3, 6 or 7, not %d", lanes);
   c->verify_lanes = lanes;
   return HBX_OK;
 }
@@ -779,12 +784,34 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n,
                          c->valid.as<uint8_t>(), own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
-    else
+    else if (lanes == 7)  // the one-lane check as one kernel (final exponentiation through call frames)
       hipLaunchKernelGGL(k_verify_shares, dim3((n + 63) / 64, p), dim3(64), 0, s, c->S.as<g1a>(),
                          c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
                          c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
                          own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
+    else {
+      // one lane per check: the Miller loops, then the final exponentiation as seven step kernels
+      // over per-lane slots (fe1d.hpp: no Fq12 ever crosses a call frame)
+      const dim3 grid((n + 63) / 64, p);
+      if (!c->fe1slot.ensure((size_t)grid.x * grid.y * 64 * 3 * FE1_WORDS * 4))
+        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory (slots)");
+      uint8_t* ctv = (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr;
+      const uint32_t me = own ? c->own_me : UINT32_MAX;
+      uint32_t* gs = c->fe1slot.as<uint32_t>();
+      hipLaunchKernelGGL(k_verify_shares_ml, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(),
+                         d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(),
+                         c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(), me, gs);
+      const uint8_t* ctok = c->ct_ok.as<uint8_t>();
+      uint8_t* vd = c->valid.as<uint8_t>();
+      hipLaunchKernelGGL(k_fe1<0>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<2>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<4>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<6>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+    }
   }
   HIPCHK(c, hipGetLastError());
   c->ct_known = true;
@@ -1038,17 +1065,9 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
                      c->coin_H.as<g2a>());
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->aux_ev[1], c->aux_stream));
-  {
-    timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
-                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
-                       UINT32_MAX, nullptr, nullptr, nullptr);
-    HIPCHK(c, hipGetLastError());
-    const uint32_t nl = count * MILLER_LINES;
-    hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
-  }
-  HIPCHK(c, hipGetLastError());
+  // the Miller lines of H' are prepared on demand by the one-lane share checks (the two-lane
+  // kernel, the default for a coin round, generates both pairs' lines itself)
+  c->coin_lines_ready = false;
   HIPCHK(c, hipStreamWaitEvent(s, c->aux_ev[1], 0));  // the true H is in
   if (h96) {
     hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count, 1u,
@@ -1080,17 +1099,71 @@ int hbx_sign(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* sig96) {
   return HBX_OK;
 }
 
+// Signature-share checks of the prepared nonces on device buffers: d_sig96 [count][n][96],
+// d_present [count][n] bytes (NULL = all present); statuses in c->coin_valid.
+static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_present, uint32_t n, uint32_t count,
+                           hipStream_t s) {
+  const size_t m = (size_t)n * count;
+  if (!c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) || !c->coin_valid.ensure(m))
+    return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
+  hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, d_sig96, m, c->coin_sig.as<g2a>(),
+                     c->coin_sig_st.as<int32_t>());
+  HIPCHK(c, hipGetLastError());
+  // two lanes per check when one lane per check would leave SIMDs idle (a coin round of 256
+  // instances at N = 128 is 512 one-lane waves on 1,024 SIMDs), or when asked for
+  // (hbx_set_verify_lanes 2); one lane otherwise
+  const size_t waves1 = (size_t)((n + 63) / 64) * count;
+  const int lanes = c->verify_lanes == 1 || c->verify_lanes == 2 ? c->verify_lanes
+                    : waves1 < (size_t)VERIFY_FILL_WAVES ? 2 : 1;
+  c->coin_lanes_used = lanes;
+  if (lanes == 1 && !c->coin_lines_ready) {
+    // H''s prepared lines for the one-lane kernel (wave-uniform loads)
+    timed t_(c, HBX_K_PREPARE_LINES, s);
+    hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
+                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
+                       UINT32_MAX, nullptr, nullptr, nullptr);
+    HIPCHK(c, hipGetLastError());
+    const uint32_t nl = count * MILLER_LINES;
+    hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
+                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
+    HIPCHK(c, hipGetLastError());
+    c->coin_lines_ready = true;
+  }
+  {
+    timed t_(c, HBX_K_VERIFY_SIG, s);
+    if (lanes == 2) {
+      const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
+      if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
+        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
+      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_Hp.as<g2a>(),
+                         c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(), d_present, n,
+                         c->coin_valid.as<uint8_t>(), c->gslot.as<uint32_t>());
+    } else {
+      hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
+                         c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
+                         c->coin_sig_st.as<int32_t>(), d_present, n, c->coin_valid.as<uint8_t>());
+    }
+  }
+  HIPCHK(c, hipGetLastError());
+  c->coin_n = n;
+  return HBX_OK;
+}
+
+static int verify_sig_check(hbx_ctx* c, uint32_t n, uint32_t count) {
+  if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
+  if (count != c->coin_I) return fail(c, HBX_E_NO_CIPHERTEXTS, "%u instances but %u nonces prepared", count, c->coin_I);
+  return HBX_OK;
+}
+
 int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* present_bits, uint32_t n, uint32_t count,
                           uint8_t* valid_bits) {
   if (!c || !sig96 || n == 0 || count == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sig_shares: bad args");
-  if (c->n_keys == 0) return fail(c, HBX_E_NO_KEYS, "hbx_set_pk_shares has not been called");
-  if (count != c->coin_I) return fail(c, HBX_E_NO_CIPHERTEXTS, "%u instances but %u nonces prepared", count, c->coin_I);
+  if (int rc = verify_sig_check(c, n, count)) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t s = pick(c, c->stream);
   stream_scope ss_{c, s};
   const size_t m = (size_t)n * count;
-  if (!c->coin_sig96.ensure(m * 96) || !c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) ||
-      !c->coin_valid.ensure(m) || (present_bits && !c->coin_present.ensure(m)))
+  if (!c->coin_sig96.ensure(m * 96) || (present_bits && !c->coin_present.ensure(m)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->coin_sig96.p, sig96, m * 96, hipMemcpyHostToDevice, s));
   std::vector<uint8_t> pres;
@@ -1099,41 +1172,29 @@ int hbx_verify_sig_shares(hbx_ctx* c, const uint8_t* sig96, const uint8_t* prese
     for (size_t k = 0; k < m; k++) pres[k] = (present_bits[k >> 3] >> (k & 7)) & 1;
     HIPCHK(c, hipMemcpyAsync(c->coin_present.p, pres.data(), m, hipMemcpyHostToDevice, s));
   }
-  hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, c->coin_sig96.as<uint8_t>(), m,
-                     c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>());
-  HIPCHK(c, hipGetLastError());
-  {
-    // two lanes per check when one lane per check would leave SIMDs idle (a coin round of 256
-    // instances at N = 128 is 512 one-lane waves on 1,024 SIMDs), or when asked for
-    // (hbx_set_verify_lanes 2); one lane otherwise
-    timed t_(c, HBX_K_VERIFY_SIG, s);
-    const size_t waves1 = (size_t)((n + 63) / 64) * count;
-    const int lanes = c->verify_lanes == 1 || c->verify_lanes == 2 ? c->verify_lanes
-                      : waves1 < (size_t)VERIFY_FILL_WAVES ? 2 : 1;
-    c->coin_lanes_used = lanes;
-    if (lanes == 2) {
-      const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
-      if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
-        return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
-      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_Hp.as<g2a>(),
-                         c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(),
-                         present_bits ? c->coin_present.as<uint8_t>() : nullptr, n, c->coin_valid.as<uint8_t>(),
-                         c->gslot.as<uint32_t>());
-    } else {
-      hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
-                         c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
-                         c->coin_sig_st.as<int32_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr, n,
-                         c->coin_valid.as<uint8_t>());
-    }
-  }
-  HIPCHK(c, hipGetLastError());
+  if (int rc = verify_sig_impl(c, c->coin_sig96.as<uint8_t>(), present_bits ? c->coin_present.as<uint8_t>() : nullptr,
+                               n, count, s))
+    return rc;
   std::vector<uint8_t> v(m);
   HIPCHK(c, hipMemcpyAsync(v.data(), c->coin_valid.p, m, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   if (valid_bits) pack_bits(v.data(), m, valid_bits);
-  c->coin_n = n;
   return HBX_OK;
 }
+
+int hbx_verify_sig_shares_d(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_present, uint32_t n, uint32_t count,
+                            uint8_t* d_status, void* stream) {
+  if (!c || !d_sig96 || n == 0 || count == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_verify_sig_shares_d: bad args");
+  if (int rc = verify_sig_check(c, n, count)) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  if (int rc = verify_sig_impl(c, d_sig96, d_present, n, count, s)) return rc;
+  if (d_status) HIPCHK(c, hipMemcpyAsync(d_status, c->coin_valid.p, (size_t)n * count, hipMemcpyDeviceToDevice, s));
+  return HBX_OK;
+}
+
+int hbx_get_coin_lanes_used(const hbx_ctx* c) { return c ? c->coin_lanes_used : 0; }
 
 int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, const uint64_t* msg_off,
                     const uint8_t* sig96, uint32_t count, uint8_t* status) {
@@ -1247,38 +1308,61 @@ int hbx_bivar_check_acks(hbx_ctx* c, const uint8_t* commit48, uint32_t p, uint32
   return HBX_OK;
 }
 
-int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96, int32_t* status,
-                           uint8_t* master_ok_bits, uint8_t* parity_bits) {
-  if (!c || !master_pk48 || t == 0 || t > (uint32_t)COMBINE_MAX_T)
-    return fail(c, HBX_E_INVALID_ARG, "hbx_combine_signatures: bad args");
+// combine_signatures + master check + parity of every prepared nonce over the valid shares of
+// the last signature-share verification (masked by d_use [I][n] when given): results in
+// coin_out96 / coin_comb_st / coin_ok / coin_par.
+static int combine_sigs_impl(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, const uint8_t* d_use, hipStream_t s) {
+  if (!master_pk48 || t == 0 || t > (uint32_t)COMBINE_MAX_T) return fail(c, HBX_E_INVALID_ARG, "hbx_combine_signatures: bad args");
   if (c->coin_n == 0) return fail(c, HBX_E_NO_CIPHERTEXTS, "no verified signature shares");
-  HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t s = pick(c, c->stream);
-  stream_scope ss_{c, s};
   const uint32_t I = c->coin_I;
+  const size_t m = (size_t)I * c->coin_n;
   if (!c->coin_comb.ensure((size_t)I * sizeof(g2a)) || !c->coin_comb_st.ensure((size_t)I * 4) ||
       !c->coin_mpk_comp.ensure(48) || !c->coin_mpk.ensure(sizeof(g1a)) || !c->coin_mpk_st.ensure(4) ||
-      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96))
+      !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96) ||
+      (d_use && !c->coin_use.ensure(m)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_signatures: out of device memory");
-  HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, s, c->coin_mpk_comp.as<uint8_t>(), 1u, c->coin_mpk.as<g1a>(),
-                     c->coin_mpk_st.as<int32_t>());
-  HIPCHK(c, hipGetLastError());
-  int32_t mst = 0;
-  HIPCHK(c, hipMemcpyAsync(&mst, c->coin_mpk_st.p, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(c, hipStreamSynchronize(s));
-  if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
+  // the master key: decoded once per distinct value (era state; checked on the host)
+  if (!c->coin_mpk_known || memcmp(c->coin_mpk48, master_pk48, 48) != 0) {
+    HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_decompress_g1, dim3(1), dim3(64), 0, s, c->coin_mpk_comp.as<uint8_t>(), 1u, c->coin_mpk.as<g1a>(),
+                       c->coin_mpk_st.as<int32_t>());
+    HIPCHK(c, hipGetLastError());
+    int32_t mst = 0;
+    HIPCHK(c, hipMemcpyAsync(&mst, c->coin_mpk_st.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (mst != HBX_PT_OK) return fail(c, HBX_E_INVALID_ARG, "master public key does not decode (status %d)", mst);
+    memcpy(c->coin_mpk48, master_pk48, 48);
+    c->coin_mpk_known = true;
+  }
+  const uint8_t* valid = c->coin_valid.as<uint8_t>();
+  if (d_use) {
+    hipLaunchKernelGGL(k_coin_use, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, valid, d_use, m,
+                       c->coin_use.as<uint8_t>());
+    HIPCHK(c, hipGetLastError());
+    valid = c->coin_use.as<uint8_t>();
+  }
   {
     // the G2 combine (waves 0..2) and the master-key identity (wave 3), one block per instance
     timed t_(c, HBX_K_COMBINE_SIGS, s);
-    hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, c->coin_valid.as<uint8_t>(),
-                       c->coin_sig.as<g2a>(), c->coin_n, t, c->pk.as<g1a>(), c->pk64.as<g1a>(), c->coin_mpk.as<g1a>(),
-                       c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
+    hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, valid, c->coin_sig.as<g2a>(), c->coin_n, t,
+                       c->pk.as<g1a>(), c->pk64.as<g1a>(), c->coin_mpk.as<g1a>(), c->coin_comb.as<g2a>(),
+                       c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
   }
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_sig_parity, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(),
-                     c->coin_comb_st.as<int32_t>(), I, c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
+  hipLaunchKernelGGL(k_sig_parity, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(),
+                     I, c->coin_par.as<uint8_t>(), c->coin_out96.as<uint8_t>());
   HIPCHK(c, hipGetLastError());
+  return HBX_OK;
+}
+
+int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96, int32_t* status,
+                           uint8_t* master_ok_bits, uint8_t* parity_bits) {
+  if (!c) return HBX_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, c->stream);
+  stream_scope ss_{c, s};
+  if (int rc = combine_sigs_impl(c, master_pk48, t, nullptr, s)) return rc;
+  const uint32_t I = c->coin_I;
   std::vector<uint8_t> ok(I), par(I);
   std::vector<int32_t> st(I);
   if (sig96) HIPCHK(c, hipMemcpyAsync(sig96, c->coin_out96.p, (size_t)I * 96, hipMemcpyDeviceToHost, s));
@@ -1289,6 +1373,21 @@ int hbx_combine_signatures(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, u
   if (status) memcpy(status, st.data(), (size_t)I * 4);
   if (master_ok_bits) pack_bits(ok.data(), I, master_ok_bits);
   if (parity_bits) pack_bits(par.data(), I, parity_bits);
+  return HBX_OK;
+}
+
+int hbx_combine_signatures_d(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t, const uint8_t* d_use, uint8_t* d_sig96,
+                             int32_t* d_status, uint8_t* d_master_ok, uint8_t* d_parity, void* stream) {
+  if (!c) return HBX_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  stream_scope ss_{c, s};
+  if (int rc = combine_sigs_impl(c, master_pk48, t, d_use, s)) return rc;
+  const uint32_t I = c->coin_I;
+  if (d_sig96) HIPCHK(c, hipMemcpyAsync(d_sig96, c->coin_out96.p, (size_t)I * 96, hipMemcpyDeviceToDevice, s));
+  if (d_status) HIPCHK(c, hipMemcpyAsync(d_status, c->coin_comb_st.p, (size_t)I * 4, hipMemcpyDeviceToDevice, s));
+  if (d_master_ok) HIPCHK(c, hipMemcpyAsync(d_master_ok, c->coin_ok.p, I, hipMemcpyDeviceToDevice, s));
+  if (d_parity) HIPCHK(c, hipMemcpyAsync(d_parity, c->coin_par.p, I, hipMemcpyDeviceToDevice, s));
   return HBX_OK;
 }
 

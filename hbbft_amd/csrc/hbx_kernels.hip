@@ -19,12 +19,13 @@
 #include "pairingd.hpp"
 #include "pairing3d.hpp"
 #include "pairing2d.hpp"
+#include "fe1d.hpp"
 #include "curve4.hpp"
 #include "wide.hpp"
 
 // Split build (tools/build.py): the kernels compile in groups, one translation unit per group
-// (-DHBX_TU=1..7: epoch, share checks, producer, wide checks, coin, broadcast, two-lane share
-// checks); TU 0 is the host
+// (-DHBX_TU=1..10: epoch, share checks, producer, wide checks, coin, broadcast, two-lane share
+// checks, the one-lane checks' final-exponentiation steps in three units); TU 0 is the host
 // API, which sees only their declarations (_kdecl.hpp, generated from these sources).
 #if !defined(HBX_TU)
 #define HBX_IN_TU(n) 1
@@ -54,6 +55,10 @@ __device__ __forceinline__ uint8_t share_precheck(int32_t dec_status, bool prese
   if (!ct_ok) return HBX_SHARE_SKIPPED_CT;
   return HBX_SHARE_VALID;
 }
+
+// Internal status of a share whose pairing check waits for its final exponentiation
+// (k_verify_shares_ml -> k_fe1<6>); never visible outside a verification call.
+constexpr uint8_t SHARE_PENDING = 0xFE;
 
 // e(PA, QA) * e(PB, QB) == 1 with identity handling (pairing with the identity is 1).
 __device__ __forceinline__ bool check2(const line_pre* LA, const g1a& PA, bool qa_inf,
@@ -469,6 +474,43 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
   if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
 }
 
+// One lane per share, the Miller loop only (k_verify_shares up to its final exponentiation): the
+// Miller value conj(f) goes to the lane's global slot F (fe1d.hpp) for the seven k_fe1 steps, the
+// share status byte is final unless it is SHARE_PENDING (k_fe1<6> decides those).
+__global__ void __launch_bounds__(64) k_verify_shares_ml(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
+                                                         const uint8_t* __restrict__ present,
+                                                         const g1a* __restrict__ pk, uint32_t n_keys,
+                                                         const g2a* __restrict__ G2pts,
+                                                         const line_block_d* __restrict__ lines,
+                                                         const uint8_t* __restrict__ ct_ok, uint32_t n,
+                                                         uint8_t* __restrict__ valid, uint32_t me,
+                                                         uint32_t* __restrict__ gslot) {
+  __shared__ uint32_t park[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // the G1 points, one slot per lane
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = blockIdx.y;
+  if (i >= n) return;
+  const size_t idx = (size_t)j * n + i;
+  uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
+                               ct_ok[j] != 0);
+  if (res == HBX_SHARE_VALID) {
+    const g1a sh = S[idx], pki = pk[i];
+    const bool skipA = sh.inf || G2pts[2 * j].inf;
+    const bool skipB = pki.inf || G2pts[2 * j + 1].inf;
+    if (!(skipA && skipB)) {
+      lds_u32* slot = (lds_u32*)(park + threadIdx.x);
+      park_put_fqd(slot, 0, fqd_from_fq(sh.x));
+      park_put_fqd(slot, 1, fqd_from_fq(sh.y));
+      park_put_fqd(slot, 2, fqd_from_fq(pki.x));
+      park_put_fqd(slot, 3, fqd_neg(fqd_from_fq(pki.y)));
+      const fq12d fd = miller_loop2_parked_d(lines[j].h, !skipA, lines[j].w, !skipB, slot);
+      uint32_t* gf = gslot + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (3 * FE1_WORDS * 64) + threadIdx.x;
+      s1_put_fq12d<64>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
+      res = SHARE_PENDING;
+    }
+  }
+  valid[idx] = res;
+}
+
 #ifndef HBX_V3_WAVES
 #define HBX_V3_WAVES 1
 #endif
@@ -502,6 +544,62 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
     if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
   }
 }
+#endif
+
+#if HBX_IN_TU(8) || HBX_IN_TU(9) || HBX_IN_TU(10)
+// The seven final-exponentiation steps of the one-lane share checks (fe1d.hpp), over the same grid
+// as k_verify_shares_ml (lane = sender i, blockIdx.y = proposer j).  Lanes whose status is not
+// SHARE_PENDING have nothing to do.  Step 6 turns SHARE_PENDING into HBX_SHARE_VALID / INVALID and,
+// in own-share mode, writes the own lane's verdict as Ciphertext::verify (k_verify_shares).
+template <int STEP>
+__global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32_t n, uint8_t* __restrict__ valid,
+                                            const uint8_t* __restrict__ ct_ok, uint32_t me,
+                                            uint8_t* __restrict__ ct_valid) {
+  __shared__ uint32_t slots[FE1_WORDS * 64];  // slot A, lane-interleaved (one wave per SIMD)
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = blockIdx.y;
+  if (i >= n) return;
+  const size_t idx = (size_t)j * n + i;
+  const uint8_t st = valid[idx];
+  if (st != SHARE_PENDING) {
+    if (STEP == FE1_STEPS - 1 && i == me && ct_valid)
+      ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : st == HBX_SHARE_VALID ? HBX_CT_VALID : HBX_CT_INVALID;
+    return;
+  }
+  lds_u32* a = (lds_u32*)(slots + threadIdx.x);
+  uint32_t* gf = gslot + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (3 * FE1_WORDS * 64) + threadIdx.x;
+  uint32_t* gt = gf + FE1_WORDS * 64;
+  uint32_t* gg = gt + FE1_WORDS * 64;
+  if (STEP == 0) {
+    fe1_step0<64, 64>(a, gf, gg);
+  } else if (STEP == 1) {
+    fe1_step_expmul<64, 64>(a, gt, gg);
+  } else if (STEP == 2) {
+    fe1_step_expmul<64, 64>(a, (uint32_t*)nullptr, gg);
+  } else if (STEP == 3) {
+    fe1_step3<64, 64>(a, gf, gg);
+  } else if (STEP == 4) {
+    fe1_step4<64, 64>(a, gf, gt);
+  } else if (STEP == 5) {
+    fe1_step5<64, 64>(a, gf, gg);
+  } else {
+    const bool v = fq12d_is_one_seq(fe1_step6<64, 64>(a, gt, gg));
+    valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+    if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+  }
+}
+// the steps compile in three translation units (tools/build.py): each is a large kernel
+#if HBX_IN_TU(8)
+template __global__ void k_fe1<0>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<4>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<6>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+#elif HBX_IN_TU(9)
+template __global__ void k_fe1<1>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<2>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+#else
+template __global__ void k_fe1<3>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<5>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+#endif
 #endif
 
 #if HBX_IN_TU(7)
@@ -1279,6 +1377,14 @@ __global__ void __launch_bounds__(256) k_gate_by_ct(uint8_t* __restrict__ valid,
 // Common Coin (reference src/common_coin.rs)
 // ----------------------------------------------------------------------------------------------
 #if HBX_IN_TU(5)
+// combine_signatures over a caller-chosen subset of the verified shares (the shares a node held
+// when try_output ran, common_coin.rs:163-190): out[k] = valid[k] where use[k], else ABSENT
+__global__ void __launch_bounds__(256) k_coin_use(const uint8_t* __restrict__ valid, const uint8_t* __restrict__ use,
+                                                  size_t m, uint8_t* __restrict__ out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  out[k] = use[k] ? valid[k] : (uint8_t)HBX_SHARE_ABSENT;
+}
 // H_i = hash_g2(nonce_i) (threshold_crypto; the nonce of agreement/mod.rs:155-165), one HASH_K-lane
 // group each.  full = 0: H'_i = h_eff P = [m] H_i (m = 3(x^2 - 1), the decryption checks' trick,
 // DESIGN.md §4.2): the coin's share checks take H' with [m] g1 on the G1 side, and the true H_i

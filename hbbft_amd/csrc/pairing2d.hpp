@@ -116,6 +116,7 @@ __device__ __forceinline__ fqd lds_get_fqd_packed(const lds_u32* base, int word)
     uint32_t d = w[wd] >> sh;
     if (sh > 4) d |= w[wd + 1] << (32 - sh);
     e.d[i] = (int32_t)(d & (uint32_t)DMASK);
+    HBX_LAUNDER(e.d[i]);
   }
   e.d[13] = (int32_t)w[12];
   return e;
@@ -261,7 +262,7 @@ __device__ __forceinline__ fq6d miller2d(const line_pre_d* LA, const fqd& sA, bo
 // 14 x 2^57, re / im below 2^62.4.  Normalised output.
 __device__ __forceinline__ fq2d cyc_pair2d(const fq2d& a, const fq2d& b, bool l1) {
   HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL();
-  int32_t p1[14], q1[14], p2[14], q2[14], p3[14], p4[14], q4[14];
+  int32_t p1[14], q1[14], p2[14], q2[14], p3[14], p4[14], q4[14], q3[14];
 #pragma unroll
   for (int i = 0; i < 14; i++) {
     const int32_t a0 = a.c0.d[i], a1 = a.c1.d[i], b0 = b.c0.d[i], b1 = b.c1.d[i];
@@ -273,8 +274,8 @@ __device__ __forceinline__ fq2d cyc_pair2d(const fq2d& a, const fq2d& b, bool l1
     p3[i] = l1 ? as : b0 + b0;
     p4[i] = l1 ? a1 + a1 : a0 + a0;
     q4[i] = l1 ? b0 : a1;
+    q3[i] = b1;
   }
-  const int32_t* q3 = b.c1.d;
   fq2d r;
   fqd_redc2(
       [&](int k, int jlo, int jhi, int64_t& X, int64_t& Y) {
@@ -340,6 +341,7 @@ __device__ __forceinline__ fqd slot_get_fqd(P base, uint32_t stride, int word) {
     uint32_t d = w[wd] >> sh;
     if (sh > 4) d |= w[wd + 1] << (32 - sh);
     e.d[i] = (int32_t)(d & (uint32_t)DMASK);
+    HBX_LAUNDER(e.d[i]);
   }
   e.d[13] = (int32_t)w[12];
   return e;

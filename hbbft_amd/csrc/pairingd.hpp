@@ -218,6 +218,7 @@ HBX_HD fq12d lds_get_fq12d(const lds_u32* base) {
       uint32_t d = w[word] >> sh;
       if (sh > 4) d |= w[word + 1] << (32 - sh);
       e[q].d[i] = (int32_t)(d & (uint32_t)DMASK);
+      HBX_LAUNDER(e[q].d[i]);
     }
     e[q].d[13] = (int32_t)w[12];
   }

@@ -52,6 +52,9 @@ EXPORTS = (
     "hbx_sign",
     "hbx_verify_sig_shares",
     "hbx_combine_signatures",
+    "hbx_verify_sig_shares_d",
+    "hbx_combine_signatures_d",
+    "hbx_get_coin_lanes_used",
     "hbx_verify_sigs",
     "hbx_bivar_rows",
     "hbx_bivar_check_acks",
@@ -146,6 +149,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_sign.argtypes = [P, u8p, u32, u8p]
     lib.hbx_verify_sig_shares.argtypes = [P, u8p, u8p, u32, u32, u8p]
     lib.hbx_combine_signatures.argtypes = [P, u8p, u32, u8p, i32p, u8p, u8p]
+    lib.hbx_verify_sig_shares_d.argtypes = [P, P, P, u32, u32, P, P]
+    lib.hbx_combine_signatures_d.argtypes = [P, u8p, u32, P, P, P, P, P, P]
+    lib.hbx_get_coin_lanes_used.argtypes = [P]
     lib.hbx_verify_sigs.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
     lib.hbx_bivar_rows.argtypes = [P, u8p, u32, u32, ctypes.c_uint64, u8p, u8p]
     lib.hbx_bivar_check_acks.argtypes = [P, u8p, u32, u32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), u64p,
@@ -229,7 +235,7 @@ class Context:
         self._check(self.lib.hbx_set_digest(self.h, variant))
 
     def set_verify_lanes(self, lanes: int):
-        """hbx_set_verify_lanes: 0 auto (default), 1, 2, 3 or 6 lanes per decryption-share check."""
+        """hbx_set_verify_lanes: 0 auto (default), 1, 2, 3, 6 or 7 (one lane, single kernel) per check."""
         self._check(self.lib.hbx_set_verify_lanes(self.h, lanes))
 
     def verify_lanes_used(self) -> int:
@@ -421,6 +427,32 @@ class Context:
         self._check(self.lib.hbx_verify_sig_shares(self.h, _u8(sigs), None if pres is None else _u8(pres), n, count,
                                                    _u8(bits)))
         return unpack_bits(bits, count * n).reshape(count, n)
+
+    def coin_lanes_used(self) -> int:
+        """hbx_get_coin_lanes_used: lanes per check of the last signature-share verification."""
+        return int(self.lib.hbx_get_coin_lanes_used(self.h))
+
+    def verify_sig_shares_d(self, d_sigs, d_present=None, d_status=None, stream=None):
+        """d_sigs: uint8[count, n, 96] device tensor; d_present / d_status: uint8[count, n] (or None)."""
+        import torch
+
+        count, n, w = d_sigs.shape
+        if w != 96 or d_sigs.dtype != torch.uint8 or not d_sigs.is_contiguous():
+            raise ValueError("verify_sig_shares_d: d_sigs must be contiguous uint8[count, n, 96]")
+        for x in (d_present, d_status):
+            if x is not None and (tuple(x.shape) != (count, n) or x.dtype != torch.uint8 or not x.is_contiguous()):
+                raise ValueError(f"verify_sig_shares_d: present/status must be contiguous uint8[{count}, {n}]")
+        opt = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        self._check(self.lib.hbx_verify_sig_shares_d(self.h, d_sigs.data_ptr(), opt(d_present), n, count,
+                                                     opt(d_status), self._stream(stream)))
+
+    def combine_signatures_d(self, master_pk48: bytes, t: int, d_use=None, d_sig=None, d_status=None, d_ok=None,
+                             d_parity=None, stream=None):
+        """hbx_combine_signatures_d: d_use uint8[count, n] (or None: every valid share)."""
+        mpk = np.frombuffer(bytes(master_pk48), dtype=np.uint8).copy()
+        opt = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        self._check(self.lib.hbx_combine_signatures_d(self.h, _u8(mpk), t, opt(d_use), opt(d_sig), opt(d_status),
+                                                      opt(d_ok), opt(d_parity), self._stream(stream)))
 
     def combine_signatures(self, master_pk48: bytes, t: int):
         """-> (sig uint8[count, 96], status int32[count], master_ok bool[count], parity bool[count])."""

@@ -68,3 +68,72 @@ def assemble(gathered: np.ndarray, n: int, world: int):
         cv.append(g[r, lay["ct_valid"][0]:lay["ct_valid"][0] + pj])
         st.append(g[r, lay["status"][0]:lay["status"][0] + 4 * pj].copy().view(np.int32))
     return np.concatenate(sv), np.concatenate(cv), np.concatenate(st)
+
+
+# ---------------------------------------------------------------------------------------------
+# Common Coin and Broadcast rounds: sharded by instance ("Coin: shard by
+# instance.  Broadcast: shard by instance (proposer)").  Rank g owns the contiguous instance range
+# instance_range(count, world, g) -- its nonces (hash_g2, lines), signature shares, combines, or
+# its proposals (encode, Merkle trees, Echo validation, decodes).  One all-gather of a fixed-size
+# slab per rank then gives every rank the whole round's result: per-share status bytes, combined
+# signatures with their master-check and parity bits (coin), or the roots, decode statuses and
+# output lengths (broadcast); payload bytes stay on the owning GPU.
+# ---------------------------------------------------------------------------------------------
+instance_range = proposer_range
+
+
+class SlabLayout:
+    """Named fields of one rank's result slab at 8-byte aligned offsets: [(name, numpy dtype,
+    shape)], shapes for the largest rank's instance count so that all slabs have one size."""
+
+    def __init__(self, fields):
+        self.fields = {}
+        pos = 0
+        for name, dt, shape in fields:
+            dt = np.dtype(dt)
+            pos = (pos + 7) // 8 * 8
+            nbytes = int(np.prod(shape)) * dt.itemsize
+            self.fields[name] = (pos, dt, tuple(shape), nbytes)
+            pos += nbytes
+        self.size = (pos + 7) // 8 * 8
+
+    def view(self, buf, name, rows=None):
+        """Typed view of field ``name`` in a uint8 buffer (numpy array or torch tensor), optionally
+        only its first ``rows`` rows."""
+        off, dt, shape, nbytes = self.fields[name]
+        part = buf[off:off + nbytes]
+        if hasattr(part, "view") and not isinstance(part, np.ndarray):  # torch
+            import torch
+
+            tdt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int32): torch.int32,
+                   np.dtype(np.int64): torch.int64}[dt]
+            v = part.view(tdt).view(shape)
+        else:
+            v = part.view(dt).reshape(shape)
+        return v if rows is None else v[:rows]
+
+
+def coin_layout(count: int, n: int, world: int) -> SlabLayout:
+    im = max_columns(count, world)
+    return SlabLayout([("share_status", np.uint8, (im, n)), ("sig", np.uint8, (im, 96)),
+                       ("comb_status", np.int32, (im,)), ("master_ok", np.uint8, (im,)),
+                       ("parity", np.uint8, (im,))])
+
+
+def broadcast_layout(count: int, world: int) -> SlabLayout:
+    im = max_columns(count, world)
+    return SlabLayout([("root", np.uint8, (im, 32)), ("decode_status", np.int32, (im,)),
+                       ("out_len", np.int64, (im,))])
+
+
+def assemble_fields(gathered, layout: SlabLayout, count: int, world: int):
+    """Gathered slabs [world, size] -> {field: array over all ``count`` instances in order}."""
+    g = np.asarray(gathered, dtype=np.uint8).reshape(world, layout.size)
+    out = {}
+    for name in layout.fields:
+        parts = []
+        for r in range(world):
+            lo, hi = instance_range(count, world, r)
+            parts.append(np.array(layout.view(g[r], name, hi - lo)))
+        out[name] = np.concatenate(parts)
+    return out

@@ -133,13 +133,16 @@ int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launch
  * ------------------------------------------------------------------------------------------- */
 int hbx_set_digest(hbx_ctx* ctx, int variant);
 /* Lanes per decryption-share check (no reference counterpart; results identical): 1 = one lane
- * per check (the throughput kernel when a launch fills the chip), 2 = a lane pair per check (the
+ * per check (the throughput path when a launch fills the chip: a Miller-loop kernel and the final
+ * exponentiation as seven step kernels over per-lane slots), 7 = one lane per check in a single
+ * kernel (the final exponentiation through call frames; kept for comparison), 2 = a lane pair per
+ * check (the
  * Fq12 state split in halves, no scratch), 3 = three cooperating lanes per check, 6 = six lanes per
  * check (the two Miller loops on two lane triplets side by side; lowest latency per check), 0 =
  * choose by launch size (default: 1 when one-lane checks fill >= 1024 waves, else 6 when six-lane
  * checks fit in 1024 waves, else 3). */
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
-/* Lanes per check the last decryption-share launch used (1, 2, 3 or 6; 0 before any launch). */
+/* Lanes per check the last decryption-share launch used (1, 2, 3, 6 or 7; 0 before any launch). */
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
 /* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
  * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over
@@ -281,6 +284,14 @@ int hbx_decrypt_shares(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint
  * hbx_combine_signatures -- PublicKeySet::combine_signatures over the first t valid shares in
  *   node-index order (src/common_coin.rs:190) + PublicKey::verify with the master key (:196) +
  *   Signature::parity (:173).  status[inst]: HBX_OK / HBX_E_NOT_ENOUGH_SHARES.
+ * Device variants (torch-style HBM buffers, `stream` as in the threshold _d calls):
+ * hbx_verify_sig_shares_d -- d_sig96 [count][n][96], d_present [count][n] bytes (NULL = all),
+ *   d_status [count][n] = HBX_SHARE_* (NULL: keep them in the context only).
+ * hbx_combine_signatures_d -- as hbx_combine_signatures over the last verification's valid shares,
+ *   restricted to d_use[inst][i] != 0 when d_use is given (the shares a node held when try_output
+ *   ran, common_coin.rs:163-190); outputs d_sig96 [I][96], d_status [I] int32, d_master_ok [I] and
+ *   d_parity [I] bytes (each may be NULL).  The master key is a host pointer (48 bytes; decoded
+ *   once per distinct value).
  * ------------------------------------------------------------------------------------------- */
 int hbx_prepare_nonces(hbx_ctx* ctx, const uint8_t* nonce_blob, const uint64_t* nonce_off, uint32_t count,
                        uint8_t* h96);
@@ -291,6 +302,15 @@ int hbx_verify_sig_shares(hbx_ctx* ctx, const uint8_t* sig96, const uint8_t* pre
 int hbx_get_sig_share_status(hbx_ctx* ctx, uint8_t* status, size_t count);
 int hbx_combine_signatures(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t, uint8_t* sig96,
                            int32_t* status, uint8_t* master_ok_bits, uint8_t* parity_bits);
+int hbx_verify_sig_shares_d(hbx_ctx* ctx, const uint8_t* d_sig96, const uint8_t* d_present, uint32_t n,
+                            uint32_t count, uint8_t* d_status, void* stream);
+int hbx_combine_signatures_d(hbx_ctx* ctx, const uint8_t* master_pk48, uint32_t t, const uint8_t* d_use,
+                             uint8_t* d_sig96, int32_t* d_status, uint8_t* d_master_ok, uint8_t* d_parity,
+                             void* stream);
+/* Lanes per check the last signature-share verification used (1 or 2; 0 before any): the coin
+ * honours hbx_set_verify_lanes 1 and 2; 0, 3, 6 and 7 choose automatically (2 when one-lane checks
+ * would fill fewer than 1024 waves, else 1). */
+int hbx_get_coin_lanes_used(const hbx_ctx* ctx);
 
 /* ---------------------------------------------------------------------------------------------
  * Dynamic HoneyBadger / key-generation signatures: threshold_crypto

@@ -307,14 +307,15 @@ def test_one_lane_combine_matches_golden(hbx_ctx, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lanes", [1, 2, 3])
+@pytest.mark.parametrize("lanes", [1, 2, 3, 7])
 @pytest.mark.parametrize("name", ["hb_epoch_n4", "hb_epoch_n7", "hb_epoch_n10", "hb_epoch_n64", "hb_cols_n256",
                                   "hb_epoch_n7_sha3"])
 def test_one_lane_checks_match_golden(hbx_ctx, name, lanes):
     """The fixtures' launches are small, so the default (auto) path above runs the six-lane
-    share check (pairing3d.hpp check2_g6d); this forces the one-lane kernel (what a full N = 256
-    epoch on one GPU uses), the two-lane kernel (pairing2d.hpp) and the three-lane kernel through
-    the same expectations, plain and own-share mode."""
+    share check (pairing3d.hpp check2_g6d); this forces the one-lane path (what a full N = 256
+    epoch on one GPU uses: the Miller kernel + the seven final-exponentiation step kernels of
+    fe1d.hpp), the single-kernel one-lane check (7), the two-lane kernel (pairing2d.hpp) and the
+    three-lane kernel through the same expectations, plain and own-share mode."""
     d = _load(name)
     _set_keys(hbx_ctx, d)
     hbx_ctx.set_verify_lanes(lanes)

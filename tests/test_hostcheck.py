@@ -168,6 +168,21 @@ def test_digit_tower_pairing_check(hc):
     assert hc.hc_miller2_digit_cmp(pa, g2, ng1, qa, ctypes.byref(chk)) == 3 and chk.value == 1
 
 
+def test_fe1_chain_matches_final_exponentiation(hc):
+    """k_fe1's five-step final exponentiation (fe1d.hpp: the Fq12 values handed between kernels
+    through packed slots, products streaming one operand from a slot) gives the same element as
+    final_exponentiation_d, for checks that hold and checks that do not (HBX_DCHECK bounds on)."""
+    rnd = random.Random(23)
+    for trial in range(4):
+        a = rnd.randrange(1, bls.R)
+        pa = bls.g1_compress(bls.g1_mul(bls.G1_GEN, a))
+        q = bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R))
+        qa = bls.g2_compress(q)
+        ng1 = bls.g1_compress(bls.g1_neg(bls.G1_GEN))
+        qb = bls.g2_compress(bls.g2_mul(q, a + (trial & 1)))  # holds for even trials
+        assert hc.hc_fe1_chain_cmp(pa, qa, ng1, qb) == (7 if trial % 2 == 0 else 3)
+
+
 def test_sha256_and_hash_g1_g2(hc):
     for n in (0, 1, 55, 56, 64, 65, 200):
         m = bytes(range(n % 251))[:n] + bytes(max(0, n - 251))

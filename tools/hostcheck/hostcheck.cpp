@@ -4,6 +4,7 @@
 #include <cstring>
 #include "../../hbbft_amd/csrc/pairing.hpp"
 #include "../../hbbft_amd/csrc/pairingd.hpp"
+#include "../../hbbft_amd/csrc/fe1d.hpp"
 #include "../../hbbft_amd/csrc/hash.hpp"
 using namespace hbx;
 extern "C" {
@@ -128,6 +129,40 @@ int hc_miller2_digit_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb
   int same_fe = 1;
   for (int i = 0; i < 12; i++) same_fe &= fq_eq(x[i], y[i]) ? 1 : 0;
   return same + 2 * same_fe;
+}
+// The final exponentiation as k_fe1's five steps (fe1d.hpp) on host slots, against
+// final_exponentiation_d on the same Miller output: 1 = the same element, + 2 if the verdicts
+// (fq12d_is_one_seq vs fq12_is_one) agree, + 4 if the check holds.
+int hc_fe1_chain_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK) return -1;
+  if (g1_decompress(pb, PB) != HBX_PT_OK) return -2;
+  if (g2_decompress(qa, QA) != HBX_PT_OK) return -3;
+  if (g2_decompress(qb, QB) != HBX_PT_OK) return -4;
+  static line_pre LA[MILLER_LINES], LB[MILLER_LINES];
+  static line_pre_d DA[MILLER_LINES], DB[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  g2_prepare_lines(QB, LB, scratch);
+  for (int i = 0; i < MILLER_LINES; i++) {
+    DA[i] = line_to_d(LA[i]);
+    DB[i] = line_to_d(LB[i]);
+  }
+  const fq12d fd = miller_loop2_d(DA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), true, DB, fqd_from_fq(PB.x),
+                                  fqd_from_fq(PB.y), true);
+  static uint32_t slot[LDS_FQ12D_DWORDS];
+  const fq12 e1 = fq12d_to_fq12(final_exponentiation_d(fd, slot));
+  // the Miller kernel's hand-over: conj(f) stored normalised in slot F
+  static uint32_t a[FE1_WORDS], gf[FE1_WORDS], gt[FE1_WORDS], gg[FE1_WORDS];
+  s1_put_fq12d<1>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
+  const fq12d e2d = fe1_chain<1, 1>(a, gf, gt, gg);
+  const fq12 e2 = fq12d_to_fq12(e2d);
+  const fq* x = &e1.c0.c0.c0;
+  const fq* y = &e2.c0.c0.c0;
+  int same = 1;
+  for (int i = 0; i < 12; i++) same &= fq_eq(x[i], y[i]) ? 1 : 0;
+  const bool v1 = fq12_is_one(e1), v2 = fq12d_is_one_seq(e2d);
+  return same + 2 * (v1 == v2 ? 1 : 0) + 4 * (v2 ? 1 : 0);
 }
 // digit-form product against the 12-limb one on canonical inputs: out = canonical a b (BE)
 void hc_fqd_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {

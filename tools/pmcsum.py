@@ -11,7 +11,7 @@ for db in sys.argv[1:]:
     for k, cn, v, nd in c.execute(q):
         rows[k.split("(")[0]][cn] = (v, nd)
 for k in sorted(rows):
-    if not k.startswith("hbx::"):
+    if "hbx::" not in k:
         continue
     items = ", ".join(f"{cn}={v / nd:.4g}" for cn, (v, nd) in sorted(rows[k].items()))
     print(f"{k}: {items}")
