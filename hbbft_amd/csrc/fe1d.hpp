@@ -224,17 +224,95 @@ HBX_HD fq12d fq12d_cyclotomic_sqr_seq(const fq12d& f) {
   return fq12d{fq6d{z0, z4, n3}, fq6d{n2, z1, z5}};
 }
 
+// ---- Karabina compressed squarings (the exp-by-|x| runs of 9, 32 and 16 squarings) ---------
+// An element of the cyclotomic subgroup is determined by four of its six Fq2 coefficients,
+// g1 = c0.c1, g2 = c0.c2, g3 = c1.c0, g5 = c1.c2, and its square's four from them with six Fq2
+// squarings (Granger-Scott: nine):
+//   g1' = 3 (g3^2 + xi g2^2) - 2 g1        g2' = 3 (g1^2 + xi g5^2) - 2 g2
+//   g3' = 6 xi g1 g5 + 2 g3                g5' = 6 g2 g3 + 2 g5
+// (2 g1 g5 = (g1 + g5)^2 - g1^2 - g5^2, 2 g2 g3 likewise).  Decompression recovers
+//   g4 = c1.c1 = (xi g5^2 + 3 g1^2 - 2 g2) / (4 g3),   g0 = c0.c0 = xi (2 g4^2 + g3 g5 - 3 g1 g2) + 1,
+// one Fq2 inversion per run (checked against the oracle's squarings, tools/hostcheck).  g3 = 0
+// makes the division impossible (an event of probability ~2^-760 per run, not reachable by
+// choosing shares); such a lane is flagged and re-checked by the single-kernel path.
+struct fq12c {
+  fq2d g1, g2, g3, g5;
+};
+HBX_HD fq2d fq2d_lin(const fq2d& a3, const fq2d& b2, bool minus) {  // reduce(3 a +/- 2 b), a, b normalised
+  const fq2d a = fq2d_add(fq2d_dbl(a3), a3);
+  const fq2d b = fq2d_dbl(b2);
+  return fq2d_reduce(minus ? fq2d_sub(a, b) : fq2d_add(a, b));
+}
+HBX_HD void karabina_sqr(fq12c& c) {
+  const fq2d s1 = fq2d_sqr(c.g1);
+  HBX_SEQ();
+  const fq2d s5 = fq2d_sqr(c.g5);
+  HBX_SEQ();
+  const fq2d x15 = fq2d_norm(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(c.g1, c.g5)), s1), s5));  // 2 g1 g5
+  HBX_SEQ();
+  const fq2d s3 = fq2d_sqr(c.g3);
+  HBX_SEQ();
+  const fq2d s2 = fq2d_sqr(c.g2);
+  HBX_SEQ();
+  const fq2d x23 = fq2d_norm(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(c.g2, c.g3)), s2), s3));  // 2 g2 g3
+  HBX_SEQ();
+  const fq2d n1 = fq2d_lin(fq2d_norm(fq2d_add(s3, fq2d_mul_xi(s2))), c.g1, true);
+  const fq2d n2 = fq2d_lin(fq2d_norm(fq2d_add(s1, fq2d_mul_xi(s5))), c.g2, true);
+  const fq2d n3 = fq2d_lin(fq2d_norm(fq2d_mul_xi(x15)), c.g3, false);
+  const fq2d n5 = fq2d_lin(x23, c.g5, false);
+  c = fq12c{n1, n2, n3, n5};
+}
+// decompressed element (reduced); `degenerate` set when g3 = 0
+HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
+  fq2d g4;
+  {
+    const fq2d t1 = fq2d_norm(fq2d_sub(fq2d_add(fq2d_dbl(fq2d_sqr(c.g1)), fq2d_sqr(c.g1)), fq2d_dbl(c.g2)));
+    HBX_SEQ();
+    const fq2d num = fq2d_reduce(fq2d_add(fq2d_mul_xi(fq2d_sqr(c.g5)), t1));
+    HBX_SEQ();
+    const fq2d den = fq2d_reduce(fq2d_dbl(fq2d_dbl(c.g3)));
+    const fqd nrm = fqd_reduce(fqd_add(fqd_sqr(den.c0), fqd_sqr(den.c1)));
+    HBX_SEQ();
+    const fq cn = fq_canon(fqd_to_fq(nrm));
+    degenerate = degenerate || fq_is_zero(cn);
+    const fqd ni = fqd_from_fq(fq_inv_i(cn));
+    HBX_SEQ();
+    g4 = fq2d_mul(num, fq2d_mul_fq(fq2d_conj(den), ni));
+  }
+  HBX_SEQ();
+  const fq2d t12 = fq2d_mul(c.g2, c.g1);
+  HBX_SEQ();
+  const fq2d s4 = fq2d_sqr(g4);
+  HBX_SEQ();
+  const fq2d t35 = fq2d_mul(c.g3, c.g5);
+  HBX_SEQ();
+  // 2 g4^2 - 3 g1 g2 + g3 g5, then xi (..) + 1
+  const fq2d u = fq2d_norm(fq2d_add(fq2d_sub(fq2d_dbl(s4), fq2d_add(fq2d_dbl(t12), t12)), t35));
+  fq2d g0 = fq2d_mul_xi(u);
+  g0.c0 = fqd_add(g0.c0, fqd_const(FQD_ONE));
+  return fq12d{fq6d{fq2d_reduce(g0), c.g1, c.g2}, fq6d{c.g3, fq2d_reduce(g4), c.g5}};
+}
+
 // r^|x| with r's value also in slot a (the base): squaring runs between the one bits of |x| (63,
-// 62, 60, 57, 48, 16), a product by the base after each run but the last.  If t3 is given, the
-// value after the first run and product (r^3) is stored there.
+// 62, 60, 57, 48, 16), a product by the base after each run but the last; the runs of 9, 32 and 16
+// squarings in compressed form.  If t3 is given, the value after the first run and product (r^3)
+// is stored there.  `degenerate`: see karabina_decompress.
 template <int S, int SG, class P, class PG>
-HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3) {
+HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3, bool& degenerate) {
   static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
 #pragma unroll 1
   for (int q = 0; q < 6; q++) {
     const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
+    if (q >= 3) {
+      fq12c c{r.c0.c1, r.c0.c2, r.c1.c0, r.c1.c2};
 #pragma unroll 1
-    for (int i = 0; i < run; i++) r = fq12d_cyclotomic_sqr_seq(r);
+      for (int i = 0; i < run; i++) karabina_sqr(c);
+      HBX_SEQ();
+      r = karabina_decompress(c, degenerate);
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < run; i++) r = fq12d_cyclotomic_sqr_seq(r);
+    }
     if (q < 5) {
       HBX_SEQ();
       r = fq12d_mul_slot<S>(r, a);
@@ -352,22 +430,22 @@ HBX_HD void fe1_step0(P a, PG gf, PG gg) {
 }
 // F1, F2: x -> conj(x^|x| x) (x = t: t^3 -> T on the way; then x = a)
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step_expmul(P a, PG gt, PG gg) {
+HBX_HD void fe1_step_expmul(P a, PG gt, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gg);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, gt);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, gt, degenerate);
   HBX_SEQ();
   r = fq12d_mul_slot<S>(r, a);
   s1_put_fq12d<SG>(gg, fq12d{r.c0, fq6d_norm(fq6d_neg(r.c1))});
 }
 // F3: b = conj(a^|x|) frob(a)  -> F
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step3(P a, PG gf, PG gg) {
+HBX_HD void fe1_step3(P a, PG gf, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gg);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
   HBX_SEQ();
   s1_frob_inplace<S, 1>(a);
   HBX_SEQ();
@@ -390,20 +468,20 @@ HBX_HD void fe1_step4(P a, PG gf, PG gt) {
 }
 // F5: u = b^|x|  -> G
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step5(P a, PG gf, PG gg) {
+HBX_HD void fe1_step5(P a, PG gf, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gf);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
   s1_put_fq12d<SG>(gg, r);
 }
 // F6: u^|x| d (= b^(x^2) d = f^(3 (p^12 - 1)/r)): == 1 iff the check holds
 template <int S, int SG, class P, class PG>
-HBX_HD fq12d fe1_step6(P a, PG gt, PG gg) {
+HBX_HD fq12d fe1_step6(P a, PG gt, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gg);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr);
+  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
   HBX_SEQ();
   s1_copy<S, SG>(a, gt);
   HBX_SEQ();
@@ -411,14 +489,14 @@ HBX_HD fq12d fe1_step6(P a, PG gt, PG gg) {
 }
 // the whole chain on one lane (host checks; the kernels run one step each)
 template <int S, int SG, class P, class PG>
-HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg) {
+HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg, bool& degenerate) {
   fe1_step0<S, SG>(a, gf, gg);
-  fe1_step_expmul<S, SG>(a, gt, gg);
-  fe1_step_expmul<S, SG>(a, (PG) nullptr, gg);
-  fe1_step3<S, SG>(a, gf, gg);
+  fe1_step_expmul<S, SG>(a, gt, gg, degenerate);
+  fe1_step_expmul<S, SG>(a, (PG) nullptr, gg, degenerate);
+  fe1_step3<S, SG>(a, gf, gg, degenerate);
   fe1_step4<S, SG>(a, gf, gt);
-  fe1_step5<S, SG>(a, gf, gg);
-  return fe1_step6<S, SG>(a, gt, gg);
+  fe1_step5<S, SG>(a, gf, gg, degenerate);
+  return fe1_step6<S, SG>(a, gt, gg, degenerate);
 }
 
 }  // namespace hbx

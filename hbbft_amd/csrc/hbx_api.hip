@@ -88,6 +88,7 @@ struct hbx_ctx {
   uint32_t n_shares = 0, verified_p = 0;
   dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
   dbuf fe1slot;  // one-lane checks: the final exponentiation's global slots F, T, G (fe1d.hpp)
+  uint32_t force_fallback = 0;  // hbx_debug_force_fallback (tests only)
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -518,6 +519,12 @@ int hbx_set_verify_lanes(hbx_ctx* c, int lanes) {
 
 int hbx_get_verify_lanes_used(const hbx_ctx* c) { return c ? c->lanes_used : 0; }
 
+int hbx_debug_force_fallback(hbx_ctx* c, uint32_t every) {
+  if (!c) return HBX_E_INVALID_ARG;
+  c->force_fallback = every;
+  return HBX_OK;
+}
+
 int hbx_set_combine_lanes(hbx_ctx* c, int lanes) {
   if (!c || (lanes != 0 && lanes != 1 && lanes != 4))
     return fail(c, HBX_E_INVALID_ARG, "hbx_set_combine_lanes: 0 (auto), 1 or 4, not %d", lanes);
@@ -789,7 +796,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
                          c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
                          own ? c->own_me : UINT32_MAX,
-                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr);
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, 0u);
     else {
       // one lane per check: the Miller loops, then the final exponentiation as seven step kernels
       // over per-lane slots (fe1d.hpp: no Fq12 ever crosses a call frame)
@@ -804,13 +811,17 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(), me, gs);
       const uint8_t* ctok = c->ct_ok.as<uint8_t>();
       uint8_t* vd = c->valid.as<uint8_t>();
-      hipLaunchKernelGGL(k_fe1<0>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<2>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<4>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
-      hipLaunchKernelGGL(k_fe1<6>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv);
+      hipLaunchKernelGGL(k_fe1<0>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<2>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<4>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<6>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      // lanes whose compressed squarings met g3 = 0 (never expected): the single-kernel check
+      hipLaunchKernelGGL(k_verify_shares, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present,
+                         c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), ctok, n, vd,
+                         me, ctv, 1u);
     }
   }
   HIPCHK(c, hipGetLastError());

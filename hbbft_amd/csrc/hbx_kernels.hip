@@ -59,6 +59,9 @@ __device__ __forceinline__ uint8_t share_precheck(int32_t dec_status, bool prese
 // Internal status of a share whose pairing check waits for its final exponentiation
 // (k_verify_shares_ml -> k_fe1<6>); never visible outside a verification call.
 constexpr uint8_t SHARE_PENDING = 0xFE;
+// A one-lane check whose compressed squarings met g3 = 0 (fe1d.hpp karabina_decompress): decided
+// again by the single-kernel check (k_verify_shares with fallback_only).
+constexpr uint8_t SHARE_FALLBACK = 0xFD;
 
 // e(PA, QA) * e(PB, QB) == 1 with identity handling (pairing with the identity is 1).
 __device__ __forceinline__ bool check2(const line_pre* LA, const g1a& PA, bool qa_inf,
@@ -443,12 +446,13 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                                                       const line_block_d* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
                                                       uint8_t* __restrict__ valid, uint32_t me,
-                                                      uint8_t* __restrict__ ct_valid) {
+                                                      uint8_t* __restrict__ ct_valid, uint32_t fallback_only) {
   __shared__ uint32_t gslots[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // final-exp base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)j * n + i;
+  if (fallback_only && valid[idx] != SHARE_FALLBACK) return;  // the lanes k_fe1 could not decide
   const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
                                      ct_ok[j] != 0);
   bool v = false;
@@ -554,7 +558,7 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
 template <int STEP>
 __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32_t n, uint8_t* __restrict__ valid,
                                             const uint8_t* __restrict__ ct_ok, uint32_t me,
-                                            uint8_t* __restrict__ ct_valid) {
+                                            uint8_t* __restrict__ ct_valid, uint32_t force_fallback) {
   __shared__ uint32_t slots[FE1_WORDS * 64];  // slot A, lane-interleaved (one wave per SIMD)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
@@ -562,7 +566,7 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   const size_t idx = (size_t)j * n + i;
   const uint8_t st = valid[idx];
   if (st != SHARE_PENDING) {
-    if (STEP == FE1_STEPS - 1 && i == me && ct_valid)
+    if (STEP == FE1_STEPS - 1 && i == me && ct_valid && st != SHARE_FALLBACK)
       ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : st == HBX_SHARE_VALID ? HBX_CT_VALID : HBX_CT_INVALID;
     return;
   }
@@ -570,35 +574,41 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   uint32_t* gf = gslot + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (3 * FE1_WORDS * 64) + threadIdx.x;
   uint32_t* gt = gf + FE1_WORDS * 64;
   uint32_t* gg = gt + FE1_WORDS * 64;
+  // force_fallback (tests only, hbx_debug_force_fallback): every force_fallback-th sender's lane
+  // takes the degenerate path, so the fallback check is exercised
+  bool degenerate = STEP == 1 && force_fallback && (i % force_fallback) == 0;
   if (STEP == 0) {
     fe1_step0<64, 64>(a, gf, gg);
   } else if (STEP == 1) {
-    fe1_step_expmul<64, 64>(a, gt, gg);
+    fe1_step_expmul<64, 64>(a, gt, gg, degenerate);
   } else if (STEP == 2) {
-    fe1_step_expmul<64, 64>(a, (uint32_t*)nullptr, gg);
+    fe1_step_expmul<64, 64>(a, (uint32_t*)nullptr, gg, degenerate);
   } else if (STEP == 3) {
-    fe1_step3<64, 64>(a, gf, gg);
+    fe1_step3<64, 64>(a, gf, gg, degenerate);
   } else if (STEP == 4) {
     fe1_step4<64, 64>(a, gf, gt);
   } else if (STEP == 5) {
-    fe1_step5<64, 64>(a, gf, gg);
+    fe1_step5<64, 64>(a, gf, gg, degenerate);
   } else {
-    const bool v = fq12d_is_one_seq(fe1_step6<64, 64>(a, gt, gg));
-    valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
-    if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+    const bool v = fq12d_is_one_seq(fe1_step6<64, 64>(a, gt, gg, degenerate));
+    if (!degenerate) {
+      valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+      if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
+    }
   }
+  if (degenerate) valid[idx] = SHARE_FALLBACK;
 }
 // the steps compile in three translation units (tools/build.py): each is a large kernel
 #if HBX_IN_TU(8)
-template __global__ void k_fe1<0>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
-template __global__ void k_fe1<4>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
-template __global__ void k_fe1<6>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<0>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
+template __global__ void k_fe1<4>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
+template __global__ void k_fe1<6>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #elif HBX_IN_TU(9)
-template __global__ void k_fe1<1>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
-template __global__ void k_fe1<2>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<1>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
+template __global__ void k_fe1<2>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #else
-template __global__ void k_fe1<3>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
-template __global__ void k_fe1<5>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*);
+template __global__ void k_fe1<3>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
+template __global__ void k_fe1<5>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #endif
 #endif
 

@@ -75,6 +75,7 @@ EXPORTS = (
     "hbx_set_verify_lanes",
     "hbx_get_verify_lanes_used",
     "hbx_set_combine_lanes",
+    "hbx_debug_force_fallback",
     "hbx_merkle_node_count",
     "hbx_merkle_build_d",
     "hbx_merkle_proofs_d",
@@ -172,6 +173,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_set_verify_lanes.argtypes = [P, ctypes.c_int]
     lib.hbx_get_verify_lanes_used.argtypes = [P]
     lib.hbx_set_combine_lanes.argtypes = [P, ctypes.c_int]
+    lib.hbx_debug_force_fallback.argtypes = [P, u32]
     lib.hbx_merkle_node_count.argtypes = [u32]
     lib.hbx_merkle_node_count.restype = u32
     lib.hbx_merkle_build_d.argtypes = [P, P, u32, u32, u32, P, P, P]
@@ -241,6 +243,11 @@ class Context:
     def verify_lanes_used(self) -> int:
         """hbx_get_verify_lanes_used: lanes per check of the last decryption-share launch."""
         return int(self.lib.hbx_get_verify_lanes_used(self.h))
+
+    def debug_force_fallback(self, every: int):
+        """hbx_debug_force_fallback (tests only): route every ``every``-th sender's one-lane check
+        through the single-kernel fallback (0 = off)."""
+        self._check(self.lib.hbx_debug_force_fallback(self.h, every))
 
     def set_combine_lanes(self, lanes: int):
         """hbx_set_combine_lanes: 0 auto (default), 1 (a lane per Lagrange term) or 4 (a quad per term)."""

@@ -144,6 +144,10 @@ int hbx_set_digest(hbx_ctx* ctx, int variant);
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
 /* Lanes per check the last decryption-share launch used (1, 2, 3, 6 or 7; 0 before any launch). */
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
+/* Tests only: in one-lane checks, treat the lane of every `every`-th sender (0 = none, the default)
+ * as if its compressed squarings had met a zero denominator, so the single-kernel fallback check
+ * decides it (a path real inputs reach with probability ~2^-760).  Results are unchanged. */
+int hbx_debug_force_fallback(hbx_ctx* ctx, uint32_t every);
 /* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
  * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over
  * one-wave blocks (k_combine_q, t <= 128), 0 = by launch size (default: 4 when the quad blocks fit

@@ -329,3 +329,25 @@ def test_one_lane_checks_match_golden(hbx_ctx, name, lanes):
             hbx_ctx.set_own_share(0, None)
     finally:
         hbx_ctx.set_verify_lanes(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hb_epoch_n10", "hb_cols_n256"])
+def test_one_lane_fallback_path_matches_golden(hbx_ctx, name):
+    """The one-lane path's fallback (a lane whose compressed squarings meet g3 = 0 is decided again
+    by the single-kernel check): forced on every third sender's lane, same statuses, plaintexts
+    and own-share ciphertext verdicts."""
+    d = _load(name)
+    _set_keys(hbx_ctx, d)
+    hbx_ctx.set_verify_lanes(1)
+    hbx_ctx.debug_force_fallback(3)
+    try:
+        _device_epoch(hbx_ctx, d, own=False)
+        hbx_ctx.set_own_share(int(d["own_me"]), d["own_sk"].tobytes())
+        try:
+            _device_epoch(hbx_ctx, d, own=True)
+        finally:
+            hbx_ctx.set_own_share(0, None)
+    finally:
+        hbx_ctx.debug_force_fallback(0)
+        hbx_ctx.set_verify_lanes(0)

@@ -319,6 +319,62 @@ int cpu_combine_sigs(const uint8_t* sig96, const uint8_t* valid, uint32_t n, uin
   return 0;
 }
 
+// PublicKeySet::decrypt (honey_badger.rs:340) as threshold_crypto runs it: per proposer, the first t
+// valid decryption shares in node order, Lagrange coefficients at 0 in Fr, sum of lambda_i S_i by
+// 255-bit double-and-add in G1, then hash_bytes (ChaCha keystream seeded by SHA-256 of the compressed
+// point) XOR V.  shares48 u8[p][n][48], valid u8[p][n]; out = plaintexts at v_off; status[j] = 0 or
+// -3 (NotEnoughShares).  BASELINE.md §2 row C3 "ms per epoch (verify + combine)".
+int cpu_combine_decrypt(const uint8_t* shares48, const uint8_t* valid, uint32_t n, uint32_t p, uint32_t t,
+                        const uint8_t* v_blob, const uint64_t* v_off, int threads, uint8_t* out, int32_t* status) {
+  std::atomic<uint32_t> next{0};
+  run_pool(threads, [&]() {
+    std::vector<uint32_t> idx;
+    for (;;) {
+      const uint32_t j = next.fetch_add(1);
+      if (j >= p) return;
+      idx.clear();
+      for (uint32_t i = 0; i < n && idx.size() < t; i++)
+        if (valid[(size_t)j * n + i] == 1) idx.push_back(i);
+      status[j] = 0;
+      if (idx.size() < t) {
+        status[j] = -3;
+        continue;
+      }
+      g1j acc = g1_identity();
+      for (uint32_t a = 0; a < t; a++) {
+        fr num = fr_from_const(FR_ONE), den = fr_from_const(FR_ONE), xa{};
+        xa.l[0] = idx[a] + 1;
+        xa = fr_to_mont(xa);
+        for (uint32_t b = 0; b < t; b++) {
+          if (b == a) continue;
+          fr xb{};
+          xb.l[0] = idx[b] + 1;
+          xb = fr_to_mont(xb);
+          num = fr_mul(num, xb);
+          den = fr_mul(den, fr_sub(xb, xa));
+        }
+        const fr lam = fr_from_mont(fr_mul(num, fr_inv(den)));
+        g1a S;
+        g1_decompress(shares48 + ((size_t)j * n + idx[a]) * 48, S);
+        acc = g1_add(acc, g1_mul_scalar(g1_from_affine(S), lam.l));
+      }
+      uint8_t comp[48], d[32];
+      g1_compress(g1_to_affine(acc), comp);
+      digest2(DIGEST_SHA256, comp, 48, nullptr, 0, d);
+      uint32_t key[8];
+      for (int q = 0; q < 8; q++)
+        key[q] = ((uint32_t)d[4 * q] << 24) | ((uint32_t)d[4 * q + 1] << 16) | ((uint32_t)d[4 * q + 2] << 8) | d[4 * q + 3];
+      const uint64_t off = v_off[j], len = v_off[j + 1] - off;
+      for (uint64_t b = 0; 16 * b < len; b++) {
+        uint32_t ks[16];
+        chacha20_block(key, b, 0, ks);
+        for (uint64_t q = 16 * b; q < len && q < 16 * b + 16; q++) out[off + q] = v_blob[off + q] ^ (uint8_t)ks[q - 16 * b];
+      }
+    }
+  });
+  return 0;
+}
+
 // ---- reed-solomon-erasure 3.1.0 shape: GF(2^8) with poly 0x11D, MUL_TABLE rows -----------------
 namespace {
 struct gf8 {

@@ -155,7 +155,9 @@ int hc_fe1_chain_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, co
   // the Miller kernel's hand-over: conj(f) stored normalised in slot F
   static uint32_t a[FE1_WORDS], gf[FE1_WORDS], gt[FE1_WORDS], gg[FE1_WORDS];
   s1_put_fq12d<1>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
-  const fq12d e2d = fe1_chain<1, 1>(a, gf, gt, gg);
+  bool degenerate = false;
+  const fq12d e2d = fe1_chain<1, 1>(a, gf, gt, gg, degenerate);
+  if (degenerate) return -5;
   const fq12 e2 = fq12d_to_fq12(e2d);
   const fq* x = &e1.c0.c0.c0;
   const fq* y = &e2.c0.c0.c0;
