@@ -121,3 +121,28 @@ def test_rs_port_matches_oracle(port, n):
     port.cpu_rs_reconstruct(work.ctypes.data, present.ctypes.data, inst, k, m, L, 2, status.ctypes.data)
     assert (status == 0).all()
     np.testing.assert_array_equal(work, want)
+
+
+@pytest.mark.parametrize("n", [4, 7, 10])
+def test_combine_decrypt_port_matches_fixture(port, n):
+    """CPU baseline row C3 (verify + combine): PublicKeySet::decrypt over the first t valid shares
+    gives the fixture's plaintexts and NotEnoughShares statuses."""
+    P, u32 = ctypes.c_void_p, ctypes.c_uint32
+    port.cpu_combine_decrypt.argtypes = [P, P, u32, u32, u32, P, P, ctypes.c_int, P, P]
+    d = dict(np.load(os.path.join(ROOT, "tests", "golden", f"hb_epoch_n{n}.npz"), allow_pickle=False))
+    p = len(d["v_off"]) - 1
+    nn = d["shares"].shape[1]
+    sh = np.ascontiguousarray(d["shares"], dtype=np.uint8)
+    valid = np.ascontiguousarray(d["expect_valid"], dtype=np.uint8)
+    v = np.ascontiguousarray(d["v_blob"], dtype=np.uint8)
+    off = np.ascontiguousarray(d["v_off"], dtype=np.uint64)
+    out = np.zeros_like(v)
+    st = np.zeros(p, dtype=np.int32)
+    assert port.cpu_combine_decrypt(sh.ctypes.data, valid.ctypes.data, nn, p, int(d["t"]), v.ctypes.data,
+                                    off.ctypes.data, 2, out.ctypes.data, st.ctypes.data) == 0
+    ok = d["expect_ct_valid"].astype(bool)
+    np.testing.assert_array_equal(st[ok], d["expect_status"][ok])
+    for j in range(p):
+        if ok[j] and d["expect_status"][j] == 0:
+            a, b = int(off[j]), int(off[j + 1])
+            assert out[a:b].tobytes() == d["expect_plain_blob"][a:b].tobytes(), j
