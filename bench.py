@@ -2,7 +2,7 @@
 other BASELINE.json configs as sub-objects of the same JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--vlen 1024] [--no-cpu-baseline]
-                    [--configs C2,C4,C5]
+                    [--configs C1,C2,C4,C5]
 
 A *step* is the crypto of one HoneyBadger epoch as one node sees it (SURVEY.md §3 stack A,
 BASELINE.json configs[2]): for every one of the N accepted proposals
@@ -12,7 +12,8 @@ BASELINE.json configs[2]): for every one of the N accepted proposals
 i.e. 65,536 share verifications + 256 ciphertext checks + 256 Lagrange combines (t = 86) + the
 hash_bytes keystream XOR, through the C ABI of libhbx.so on device-resident inputs.
 
-``configs`` (single GPU, rank 0 only): C2 (an N=64 epoch, BASELINE config 1), C4 (Common Coin,
+``configs`` (single GPU, rank 0 only): C1 (the N=10 node-epoch of the simulation example, BASELINE
+config 0, in ms), C2 (an N=64 epoch, BASELINE config 1), C4 (Common Coin,
 256 instances at N=128, config 3) and C5 (Broadcast, 128 x 1 MiB proposals at N=128, both Merkle
 digests, config 4), each with its own value, roofline and CPU baseline.
 
@@ -95,7 +96,7 @@ def parse(argv=None):
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
-    ap.add_argument("--configs", default="C2,C4,C5",
+    ap.add_argument("--configs", default="C1,C2,C4,C5",
                     help="secondary BASELINE configs in the same line ('' for none); at --gpus > 1 (strong) C4 "
                          "and C5 run sharded by instance")
     return ap.parse_args(argv)
@@ -165,6 +166,7 @@ def cpu_lib():
     lib.cpu_combine_sigs.argtypes = [P, P, u32, u32, u32, P, P, P, i32, P, P]
     lib.cpu_rs_encode.argtypes = [P, u32, u32, u32, u32, i32]
     lib.cpu_rs_reconstruct.argtypes = [P, P, u32, u32, u32, u32, i32, P]
+    lib.cpu_combine_decrypt.argtypes = [P, P, u32, u32, u32, P, P, i32, P, P]
     return lib
 
 
@@ -266,14 +268,35 @@ def cpu_baseline_dec(ep, seconds: float):
         dq = run(jobs, qc, True)
         rows["b_hoisted_fused_quota_cores"] = {"value": round(len(jobs) / dq, 1), "cores": qc,
                                                "sample": f"same sample in {dq:.1f} s; cgroup cpu.max allows {qc} CPUs"}
-    return dict(value=round(len(jobs) / db, 1), unit="share verifies/s", cores=threads, kind="port",
-                host=host,
+    best = max(("b_hoisted_fused_all_cores", "b_hoisted_fused_quota_cores"),
+               key=lambda r: rows[r]["value"] if r in rows else -1)
+    # PublicKeySet::decrypt (honey_badger.rs:340) of a sample of proposers on the best row's threads:
+    # Lagrange combine of the first t valid shares + hash_bytes keystream XOR, checked against the
+    # contributions; the epoch row adds the share checks of the whole epoch at the best rate
+    bt = rows[best]["cores"]
+    pc = max(1, min(p, 2 * bt))
+    valid = np.ascontiguousarray(~ep["corrupt"], dtype=np.uint8)
+    outp = np.zeros_like(v)
+    stc = np.zeros(p, dtype=np.int32)
+    t0 = time.perf_counter()
+    lib.cpu_combine_decrypt(sh.ctypes.data, valid.ctypes.data, n, pc, ep["t"], v.ctypes.data, off.ctypes.data, bt,
+                            outp.ctypes.data, stc.ctypes.data)
+    dc = time.perf_counter() - t0
+    assert (stc[:pc] == 0).all() and all(outp[off[j]:off[j + 1]].tobytes() == ep["msgs"][j] for j in range(pc)), \
+        "CPU combine / decrypt"
+    comb_ms = dc / pc * p * 1e3
+    rows["c_combine_decrypt"] = {"ms_per_epoch": round(comb_ms, 1), "cores": bt, "t": int(ep["t"]),
+                                 "sample": f"{pc} proposers in {dc:.2f} s, scaled to {p}"}
+    rows["epoch_verify_plus_combine"] = {"ms_per_epoch": round(p * n / rows[best]["value"] * 1e3 + comb_ms, 1),
+                                         "cores": bt, "note": f"{p * n} checks at row {best} + row c_combine_decrypt"}
+    return dict(value=rows[best]["value"], unit="share verifies/s", cores=rows[best]["cores"], kind="port",
+                host=host, best_row=best, cgroup_cpus=qc,
                 rows=rows,
                 sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']} (nproc {host['nproc']}, "
-                       f"affinity {host['affinity']}): (b) {threads} std::threads, hash_g1_g2 + lines hoisted per "
-                       f"proposer, one 2-pair Miller loop + one final exponentiation per share, {cols} whole proposer "
-                       f"columns of the N={n} epoch in {db:.1f} s; (a) 1 thread, the reference's per-share shape, "
-                       f"{na} shares; a restatement, not the reference binary (no Rust toolchain)")
+                       f"affinity {host['affinity']}, cgroup quota {qc or 'none'} CPUs): value = row {best}; (b) "
+                       f"hash_g1_g2 + lines hoisted per proposer, one 2-pair Miller loop + one final exponentiation "
+                       f"per share, {cols} whole proposer columns of the N={n} epoch; (a) 1 thread, the reference's "
+                       f"per-share shape, {na} shares; a restatement, not the reference binary (no Rust toolchain)")
 
 
 class EpochBench:
@@ -344,8 +367,10 @@ def verify_roofline(shares: int, ms_kernel: float, kernel: str, traffic=None):
                      "note": "the current code's own Fq-mul count (tools/opcount), reported beside the frozen unit"}}
     if traffic:
         r["traffic"] = traffic["bytes_per_launch"]
-        r["traffic_note"] = (f"PMC FETCH_SIZE+WRITE_SIZE per launch of {traffic['kernel']} at N=256 "
-                             f"({traffic['source']}, commit {traffic.get('commit', '?')}); algorithmic ~1.2e7 B")
+        r["traffic_note"] = (f"PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE per share-check region at N=256, summed over "
+                             f"{traffic['kernel']} ({traffic['source']}, commit {traffic.get('commit', '?')}); "
+                             f"algorithmic ~1.2e7 B of inputs + 3 Fq12 slots per check written and read "
+                             f"(~0.5e9 B at N=256)")
     return r
 
 
@@ -391,6 +416,73 @@ def in_flight(args, eb: EpochBench, dev, torch, Context, verifies):
         c.close()
     return {"epochs": epochs, "in_flight": F, "ms_per_epoch": round(elapsed / epochs * 1e3, 3),
             "value": round(verifies * epochs / elapsed, 1), "unit": "share verifies/s"}
+
+
+def config_c1(args, dev, torch, Context):
+    """BASELINE config 0 (``examples/simulation.rs``, 10 nodes): the crypto of one node-epoch at
+    N=10 -- 10 Ciphertext::verify, 90 decryption-share verifies, 10 combines (t=4) + decrypt -- on
+    one GPU (one hbx_decrypt_epoch_d call) and on one CPU thread in the reference's shape (the
+    simulator runs every node as a single-threaded state machine).  The network simulation itself
+    (message delays, bandwidth) is out of scope."""
+    n = 10
+    stream = torch.cuda.Stream(dev)
+    with Context(dev.index or 0) as ctx:
+        ep = make_epoch(ctx, n, 0, n, args.vlen, args.corrupt_every)
+        eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share)
+        eb.bind_outputs(torch.zeros(n * n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
+                        torch.zeros(n, dtype=torch.int32, device=dev))
+        for _ in range(max(args.warmup, 1)):
+            eb.step()
+        torch.cuda.synchronize(dev)
+        steps = max(args.steps, 10)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+        wall = []
+        for k in range(steps):
+            t0 = time.perf_counter()
+            eb.step(ev[k])
+            torch.cuda.synchronize(dev)
+            wall.append(time.perf_counter() - t0)
+        eb.check(0)
+    res = {"workload": f"node-epoch crypto at N={n} (simulation example's 10 nodes): {n} Ciphertext::verify + "
+                       f"{n * (n - 1)} decryption-share verifies + {n} combines (t={ep['t']}) + decrypt, |v|={args.vlen} B",
+           "value": round(1e3 * float(np.mean(wall)), 3), "unit": "ms per node-epoch (wall, one call, synchronised)",
+           "higher_is_better": False,
+           "epoch_ms_hip_events": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), 3),
+           "note": "latency-bound: 100 checks occupy 100 lanes; the chain of dependent stages sets the time"}
+    if not args.no_cpu_baseline:
+        lib = cpu_lib()
+        cts = ep["cts"]
+        pk = np.ascontiguousarray(ep["pk_shares"], dtype=np.uint8)
+        u = np.stack([np.frombuffer(c[0], dtype=np.uint8) for c in cts])
+        w = np.stack([np.frombuffer(c[2], dtype=np.uint8) for c in cts])
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(c[1]) for c in cts])
+        v = np.frombuffer(b"".join(c[1] for c in cts), dtype=np.uint8).copy()
+        sh = np.ascontiguousarray(ep["shares"], dtype=np.uint8)
+        kk = np.arange(n * n, dtype=np.uint64)
+        jobs = np.stack([kk // n, kk % n], axis=1).astype(np.uint32)
+        out = np.zeros(len(jobs), dtype=np.uint8)
+        t0 = time.perf_counter()
+        lib.cpu_verify_dec_shares(pk.ctypes.data, n, u.ctypes.data, v.ctypes.data, off.ctypes.data, w.ctypes.data,
+                                  sh.ctypes.data, jobs.ctypes.data, len(jobs), 1, out.ctypes.data)
+        dv = time.perf_counter() - t0
+        assert (out.astype(bool) == ~ep["corrupt"].reshape(-1)).all(), "CPU C1 checks"
+        plain = np.zeros_like(v)
+        st = np.zeros(n, dtype=np.int32)
+        t0 = time.perf_counter()
+        lib.cpu_combine_decrypt(sh.ctypes.data, out.ctypes.data, n, n, ep["t"], v.ctypes.data, off.ctypes.data, 1,
+                                plain.ctypes.data, st.ctypes.data)
+        dc = time.perf_counter() - t0
+        assert (st == 0).all() and all(plain[off[j]:off[j + 1]].tobytes() == ep["msgs"][j] for j in range(n)), "CPU C1 decrypt"
+        host = host_info()
+        res["cpu_baseline"] = {"value": round((dv + dc) * 1e3, 1), "unit": "ms per node-epoch", "cores": 1, "kind": "port",
+                               "higher_is_better": False, "host": host,
+                               "rows": {"checks_ms": round(dv * 1e3, 1), "combine_decrypt_ms": round(dc * 1e3, 1)},
+                               "sample": f"the whole N={n} node-epoch on 1 thread, reference shape (per-share hash_g1_g2 "
+                                         f"+ two pairings; {n * n} two-pairing checks: the {n} Ciphertext::verify have the "
+                                         f"shape of a share check) + {n} combines; tools/cpu_baseline/cpu_port.cpp on "
+                                         f"{host['model']}"}
+    return res
 
 
 def config_c2(args, dev, torch, Context):
@@ -548,26 +640,39 @@ def cpu_baseline_coin(pk, nonces, sigs, corrupt, master_pk, t, seconds):
     kk = np.arange(rows * n, dtype=np.uint64)
     jobs = np.stack([kk // n, kk % n], axis=1).astype(np.uint32)
     db = run(jobs, threads, 1)
-    # combine_signatures + master verify + parity of the sampled instances, all cores
+    brow = {"b_hoisted_fused_all_cores": (len(jobs) / db, threads)}
+    qc = quota_cores()
+    if qc:
+        dq = run(jobs, qc, 1)
+        brow["b_hoisted_fused_quota_cores"] = (len(jobs) / dq, qc)
+    best = max(brow, key=lambda r: brow[r][0])
+    threads_c = brow[best][1]
+    # combine_signatures + master verify + parity of the sampled instances, best row's threads
     valid = np.ascontiguousarray(~corrupt, dtype=np.uint8)
     ok = np.zeros(inst, dtype=np.uint8)
     par = np.zeros(inst, dtype=np.uint8)
     mpk = np.frombuffer(master_pk, dtype=np.uint8).copy()
     t0 = time.perf_counter()
     lib.cpu_combine_sigs(sig.ctypes.data, valid.ctypes.data, n, rows, t, mpk.ctypes.data, blob.ctypes.data,
-                         off.ctypes.data, threads, ok.ctypes.data, par.ctypes.data)
+                         off.ctypes.data, threads_c, ok.ctypes.data, par.ctypes.data)
     dc = time.perf_counter() - t0
     assert ok[:rows].all(), "CPU combine / master verification"
     host = host_info()
-    return dict(value=round(len(jobs) / db, 1), unit="sig-share verifies/s", cores=threads, kind="port", host=host,
-                rows={"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
-                                                    "sample": f"{na} shares in {da:.1f} s"},
-                      "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
-                                                    "single_thread": round(1.0 / tb1, 2),
-                                                    "sample": f"{rows} instances x {n} shares in {db:.1f} s"},
-                      "combine_master_parity_all_cores": {"ms_per_256_instances": round(dc / rows * 256 * 1e3, 1),
-                                                          "sample": f"{rows} instances in {dc:.2f} s"}},
-                sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']}: (a) 1 thread, hash_g2 per "
+    out_rows = {"a_reference_shape_1thread": {"value": round(na / da, 1), "cores": 1,
+                                              "sample": f"{na} shares in {da:.1f} s"},
+                "b_hoisted_fused_all_cores": {"value": round(len(jobs) / db, 1), "cores": threads,
+                                              "single_thread": round(1.0 / tb1, 2),
+                                              "sample": f"{rows} instances x {n} shares in {db:.1f} s"},
+                "combine_master_parity": {"ms_per_256_instances": round(dc / rows * 256 * 1e3, 1), "cores": threads_c,
+                                          "sample": f"{rows} instances in {dc:.2f} s"}}
+    if qc:
+        out_rows["b_hoisted_fused_quota_cores"] = {"value": round(brow["b_hoisted_fused_quota_cores"][0], 1),
+                                                   "cores": qc, "sample": f"same sample; cgroup cpu.max allows {qc} CPUs"}
+    out_rows["round_verify_plus_combine"] = {"ms_per_round": round((inst * n / brow[best][0] + dc / rows * inst) * 1e3, 1),
+                                             "cores": threads_c}
+    return dict(value=round(brow[best][0], 1), unit="sig-share verifies/s", cores=brow[best][1], kind="port",
+                host=host, best_row=best, cgroup_cpus=qc, rows=out_rows,
+                sample=f"tools/cpu_baseline/cpu_port.cpp (g++ -O3) on {host['model']}: value = row {best}; (a) 1 thread, hash_g2 per "
                        f"share with pairing 0.14's cofactor multiplication + two pairings; (b) {threads} threads, "
                        f"H lines per instance + one mixed Miller loop + one final exponentiation per share; a "
                        f"restatement, not the reference binary")
@@ -755,6 +860,46 @@ def cpu_merkle_root(shards, variant):
     return _tree_root([leaf(i) for i in range(n)], node)
 
 
+def _tree_levels(leaf_hashes, node):
+    levels = [list(leaf_hashes)]
+    while len(levels[-1]) > 1:
+        lv = levels[-1]
+        nxt = [node(lv[i], lv[i + 1]) for i in range(0, len(lv) - 1, 2)]
+        if len(lv) % 2:
+            nxt.append(lv[-1])
+        levels.append(nxt)
+    return levels
+
+
+def cpu_proofs(shards):
+    """Proofs (index, shard, sibling path, root) of every leaf of one SHA-256 tree, as
+    MerkleTree::gen_proof gives them (an unpaired last node moves up unchanged: no sibling)."""
+    n = shards.shape[0]
+    leaf = [hashlib.sha256(b"\x00" + bytes([i & 0xFF]) + shards[i].tobytes()).digest() for i in range(n)]
+    levels = _tree_levels(leaf, lambda a, b: hashlib.sha256(b"\x01" + a + b).digest())
+    out = []
+    for i in range(n):
+        path, q = [], i
+        for lv in levels[:-1]:
+            sib = q ^ 1
+            if sib < len(lv):
+                path.append((q & 1, lv[sib]))
+            q >>= 1
+        out.append((i, shards[i].tobytes(), path))
+    return out, levels[-1][0]
+
+
+def cpu_validate(proofs, root):
+    """Proof::validate (broadcast.rs:451) of each proof: leaf hash, then one node hash per sibling."""
+    ok = 0
+    for i, value, path in proofs:
+        h = hashlib.sha256(b"\x00" + bytes([i & 0xFF]) + value).digest()
+        for right, sib in path:
+            h = hashlib.sha256(b"\x01" + (sib + h if right else h + sib)).digest()
+        ok += h == root
+    return ok
+
+
 def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
     """C5 on host cores: reed-solomon-erasure's table-driven encode / reconstruct
     (tools/cpu_baseline/cpu_port.cpp) and the Merkle trees with OpenSSL's SHA-256 / SHA3-256
@@ -799,6 +944,25 @@ def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
         rts = list(pool.map(lambda j: cpu_merkle_root(many[j], "sha256"), range(cnt)))
     mkb = time.perf_counter() - t0
     assert all(rts[j] == roots_by["sha256"][j].tobytes() for j in range(cnt)), "CPU Merkle roots (b)"
+    # reconstruct with the last f shards missing, all cores
+    presb = np.ones((cnt, n), dtype=np.uint8)
+    presb[:, n - (n - k) // 2:] = 0
+    workb = many.copy()
+    workb[presb == 0] = 0
+    stb = np.zeros(cnt, dtype=np.int32)
+    t0 = time.perf_counter()
+    lib.cpu_rs_reconstruct(workb.ctypes.data, presb.ctypes.data, cnt, k, m, L, threads, stb.ctypes.data)
+    recb = time.perf_counter() - t0
+    assert (stb == 0).all() and np.array_equal(workb, many), "CPU reconstruct (b)"
+    del workb
+    # Echo branch verification: every (instance, sender) proof of the sample, all cores
+    pr = [cpu_proofs(many[j]) for j in range(cnt)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as pool:
+        oks = list(pool.map(lambda j: cpu_validate(pr[j][0], pr[j][1]), range(cnt)))
+    vb = time.perf_counter() - t0
+    assert sum(oks) == cnt * n, "CPU Proof::validate"
+    del pr
     prop = payload.shape[1]
     host = host_info()
     gbps = lambda b, s: round(b / s / 1e9, 3)  # noqa: E731
@@ -811,7 +975,11 @@ def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
                                     "ms_per_instance_encode_roots_decode": round((enc1 + mk1 + dec1) * 1e3, 1)},
                       "b_all_cores": {"rs_encode_GBps_hbm_equiv": gbps(cnt * (k + m) * L, encb),
                                       "merkle_sha256_GBps": gbps(cnt * n * (L + 1), mkb),
-                                      "sample": f"{cnt} instances on {threads} threads"}},
+                                      "rs_reconstruct_GBps_hbm_equiv": gbps(cnt * (k + m) * L, recb),
+                                      "reconstruct_ms_per_instance": round(recb / cnt * 1e3, 2),
+                                      "branch_verify_GBps_hashed": gbps(cnt * n * (L + 1), vb),
+                                      "branch_verify_proofs_per_s": round(cnt * n / vb, 1),
+                                      "sample": f"{cnt} instances on {threads} threads ({cnt * n} Echo proofs)"}},
                 sample=f"RS: tools/cpu_baseline/cpu_port.cpp, reed-solomon-erasure 3.1.0's MUL_TABLE shape "
                        f"(g++ -O3); Merkle: hashlib (OpenSSL) SHA-256 / SHA3-256; {host['model']}, nproc "
                        f"{host['nproc']}; a restatement, not the reference binary")
@@ -1023,7 +1191,9 @@ def main():
     kern = eb.kernel_ms()
     ctx.set_timing(False)
     lanes = ctx.verify_lanes_used()
-    kname = {1: "k_verify_shares", 2: "k_verify_shares2", 3: "k_verify_shares3", 6: "k_verify_shares6"}.get(lanes, "k_verify_shares")
+    kname = {1: "k_verify_shares_ml + k_fe1<0..6> (+ k_verify_shares for fallback lanes; one timed region)",
+             2: "k_verify_shares2", 3: "k_verify_shares3", 6: "k_verify_shares6",
+             7: "k_verify_shares (single kernel)"}.get(lanes, "k_verify_shares")
     traffic = traffic_record() if (n == 256 and pj == 256) else None
     res = {
         "metric": "BLS12-381 share verifies/sec (node) at N=256; crypto ms per HB epoch",
@@ -1059,7 +1229,7 @@ def main():
     if rank == 0 and world == 1 and args.shard_of <= 1 and args.configs:
         cfgs = {}
         for name in [c.strip().upper() for c in args.configs.split(",") if c.strip()]:
-            fn = {"C2": config_c2, "C4": config_c4, "C5": config_c5}.get(name)
+            fn = {"C1": config_c1, "C2": config_c2, "C4": config_c4, "C5": config_c5}.get(name)
             if fn is None:
                 raise SystemExit(f"unknown config {name}")
             cfgs[name] = fn(args, dev, torch, Context)

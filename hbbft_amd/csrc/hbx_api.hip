@@ -59,6 +59,7 @@ struct hbx_ctx {
   hipStream_t stream = nullptr;
   hipStream_t aux_stream = nullptr;      // side work of hbx_prepare_nonces (the true H)
   hipEvent_t aux_ev[2] = {nullptr, nullptr};
+  hipEvent_t coin_ready_ev = nullptr;  // end of hbx_prepare_nonces' work: later coin calls on any stream wait on it
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
   int merkle = 0;                     // hbx_set_merkle_digest: HBX_MERKLE_*
@@ -491,6 +492,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   (void)hipEventDestroy(c->ev_last);
   if (c->aux_ev[0]) (void)hipEventDestroy(c->aux_ev[0]);
   if (c->aux_ev[1]) (void)hipEventDestroy(c->aux_ev[1]);
+  if (c->coin_ready_ev) (void)hipEventDestroy(c->coin_ready_ev);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -655,8 +657,12 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     timed t_(c, HBX_K_PREPARE_LINES, s);
     const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
     const bool own_entry = m_early && me_early != UINT32_MAX;
-    // grouped addition steps only for small launches (an epoch shard): see g2_raw_lines_group
-    auto kpl = p <= 64 ? k_prepare_lines<true> : k_prepare_lines<false>;
+    // grouped addition steps (g2_raw_lines_group) only when the epoch's one-lane share checks would
+    // not fill the chip -- the fill test the check launch uses: their larger register footprint
+    // slowed two full N=256 epochs in flight 28.2 -> 32.5 ms per epoch (profiles/r03n_bisect_*)
+    const size_t senders = early_n ? early_n : c->n_keys;
+    const bool grouped = senders ? ((size_t)p * senders + 63) / 64 < (size_t)VERIFY_FILL_WAVES : p <= 64;
+    auto kpl = grouped ? k_prepare_lines<true> : k_prepare_lines<false>;
     hipLaunchKernelGGL(kpl, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
@@ -1058,6 +1064,9 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
   if (total) HIPCHK(c, hipMemcpyAsync(c->coin_blob.p, nonce_blob, total, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->coin_off.p, nonce_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
+  // the caller's host buffers are free once the uploads are done; the hashing itself is enqueued
+  // and the call returns without waiting for it (unless h96 asks for the hashes)
+  HIPCHK(c, hipStreamSynchronize(s));
   {
     timed t_(c, HBX_K_HASH_NONCES, s);
     hipLaunchKernelGGL(k_hash_nonces, dim3((unsigned)(((size_t)count * HASH_K + 63) / 64)), dim3(64), 0, s, c->coin_blob.as<uint8_t>(),
@@ -1085,8 +1094,10 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
                        c->coin_out96.as<uint8_t>());
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h96, c->coin_out96.p, (size_t)count * 96, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
   }
-  HIPCHK(c, hipStreamSynchronize(s));
+  if (!c->coin_ready_ev) HIPCHK(c, hipEventCreateWithFlags(&c->coin_ready_ev, hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(c->coin_ready_ev, s));
   c->coin_I = count;
   return HBX_OK;
 }
@@ -1117,6 +1128,7 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
   const size_t m = (size_t)n * count;
   if (!c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) || !c->coin_valid.ensure(m))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
+  if (c->coin_ready_ev) HIPCHK(c, hipStreamWaitEvent(s, c->coin_ready_ev, 0));  // the nonces' hashes are in
   hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, d_sig96, m, c->coin_sig.as<g2a>(),
                      c->coin_sig_st.as<int32_t>());
   HIPCHK(c, hipGetLastError());
@@ -1332,6 +1344,7 @@ static int combine_sigs_impl(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t,
       !c->coin_ok.ensure(I) || !c->coin_par.ensure(I) || !c->coin_out96.ensure((size_t)I * 96) ||
       (d_use && !c->coin_use.ensure(m)))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_combine_signatures: out of device memory");
+  if (c->coin_ready_ev) HIPCHK(c, hipStreamWaitEvent(s, c->coin_ready_ev, 0));
   // the master key: decoded once per distinct value (era state; checked on the host)
   if (!c->coin_mpk_known || memcmp(c->coin_mpk48, master_pk48, 48) != 0) {
     HIPCHK(c, hipMemcpyAsync(c->coin_mpk_comp.p, master_pk48, 48, hipMemcpyHostToDevice, s));

@@ -1,7 +1,11 @@
 """HBM bytes per launch of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE), as
 the JSON record bench.py's `traffic` field reads (profiles/<tag>_pmc_hbm.json).
 
-    python tools/pmc_json.py <fetch results.db> <write results.db> <kernel> <commit> > out.json
+    python tools/pmc_json.py <fetch results.db> <write results.db> <kernel>[,<kernel>...] <commit> > out.json
+
+Several comma-separated kernel names make one region (the one-lane share check is the Miller
+kernel + seven step kernels + the fallback launch): its bytes are the sum of each kernel's bytes
+per launch.
 
 Units and the gfx950 correction follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide reads
@@ -25,13 +29,24 @@ def per_launch(db, counter, kernel):
 
 def main():
     fdb, wdb, kernel, commit = sys.argv[1:5]
-    f_kib, nf = per_launch(fdb, "FETCH_SIZE", kernel)
-    w_kib, nw = per_launch(wdb, "WRITE_SIZE", kernel)
+    f_kib = w_kib = 0.0
+    nf, nw = [], []
+    parts = {}
+    for k in kernel.split(","):
+        fk, a = per_launch(fdb, "FETCH_SIZE", k)
+        wk, b = per_launch(wdb, "WRITE_SIZE", k)
+        f_kib += fk
+        w_kib += wk
+        nf.append(a)
+        nw.append(b)
+        parts[k] = round(2 * fk * 1024 + wk * 1024)
+    nf, nw = (nf[0], nw[0]) if len(nf) == 1 else (nf, nw)
     fetch = 2 * f_kib * 1024
     write = w_kib * 1024
     print(json.dumps({"kernel": kernel, "bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
                       "write_bytes": round(write), "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
                       "launches": [nf, nw], "fetch_correction": 2, "commit": commit,
+                      **({"parts": parts} if len(parts) > 1 else {}),
                       "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH doubled (gfx950)"}))
 
 
