@@ -155,6 +155,23 @@ def traffic_record():
     return rec
 
 
+def c5_traffic():
+    """Newest PMC records of the C5 kernels (profiles/*_pmc_c5.jsonl): {kernel: record}."""
+    import glob
+
+    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_c5.jsonl")))
+    if not recs:
+        return {}
+    out = {}
+    with open(recs[-1]) as fh:
+        for line in fh:
+            if line.strip():
+                r = json.loads(line)
+                r["source"] = os.path.relpath(recs[-1], ROOT)
+                out[r["kernel"]] = r
+    return out
+
+
 def cpu_lib():
     import ctypes
 
@@ -575,7 +592,7 @@ def config_c4(args, dev, torch, Context):
             torch.cuda.synchronize(dev)
             wall.append(time.perf_counter() - t0)
         kern = {}
-        for name in ("hash_nonces", "prepare_lines", "verify_sig", "combine_sigs"):
+        for name in ("hash_nonces", "prepare_lines", "decode_sigs", "verify_sig", "combine_sigs"):
             ms_, cnt_ = ctx.kernel_time(name)
             kern[name] = round(ms_ / max(cnt_, 1), 3) if cnt_ else 0.0
         ctx.set_timing(False)
@@ -587,7 +604,7 @@ def config_c4(args, dev, torch, Context):
     kms = kern["verify_sig"]
     achieved = inst * n * VSIG_FQMUL * MADS_PER_FQMUL / (kms * 1e-3) / 1e12
     achieved_op = inst * n * OPCOUNT_VSIG * MADS_PER_FQMUL / (kms * 1e-3) / 1e12
-    round_kernels = kern["hash_nonces"] + kern["prepare_lines"] + kern["verify_sig"] + kern["combine_sigs"]
+    round_kernels = sum(kern.values())
     res = {"workload": f"CommonCoin N={n} x {inst} instances: {inst * n} signature-share verifies + {inst} "
                        f"combine_signatures (t={t}) + master verifies + parities",
            "value": round(inst * n / (kms * 1e-3), 1), "unit": "sig-share verifies/s (verify kernel, HIP events)",
@@ -746,6 +763,8 @@ def config_c5(args, dev, torch, Context):
             roots_by[name] = roots.cpu().numpy().copy()
             ms = {key: float(np.mean(v)) for key, v in res.items()}
             leaf_bytes = inst * n * (L + 1)
+            pmc = c5_traffic()
+            kleaf = "k_merkle_leaves" + ("_sha256" if name == "sha256" else "_sha3")
             rs_bytes = inst * (k + m) * L  # k L read + m L written per instance
             ml = ml_ms / max(ml_cnt, 1)
             variants[name] = {
@@ -756,7 +775,9 @@ def config_c5(args, dev, torch, Context):
                 "merkle_leaves_GBps": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),
                 "roofline": {"bound": "hbm", "achieved": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),
                              "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(leaf_bytes / (ml * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                             "traffic": None, "kernel": "k_merkle_leaves" + ("_sha256" if name == "sha256" else "_sha3"),
+                             "traffic": pmc.get(kleaf, {}).get("bytes_per_launch"), "kernel": kleaf,
+                             "traffic_note": (f"PMC FETCH_SIZE (x2) + WRITE_SIZE per launch, {pmc[kleaf]['source']}"
+                                              if kleaf in pmc else None),
                              "work": f"{inst} x {n} leaves of {L + 1} B hashed per launch"},
             }
             variants[name]["node_epoch"] = echo_epoch(ctx, torch, dev, stream, shards, roots, present, k, m, steps)
@@ -769,7 +790,11 @@ def config_c5(args, dev, torch, Context):
                     "roofline": {"bound": "valu (v_perm_b32 table lookups)", "achieved": round(rs_bytes / (enc * 1e-3) / 1e9, 1),
                                  "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(rs_bytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                  "valu_frac": round(enc_valu / (enc * 1e-3) / PEAK_VALU_OPS, 3),
-                                 "valu_floor_ms": round(enc_valu / PEAK_VALU_OPS * 1e3, 3), "traffic": None,
+                                 "valu_floor_ms": round(enc_valu / PEAK_VALU_OPS * 1e3, 3),
+                                 "traffic": pmc.get("k_rs_code_perm", {}).get("bytes_per_launch"),
+                                 "traffic_note": ("PMC per launch averaged over the run's encode AND reconstruct "
+                                                  f"launches ({pmc['k_rs_code_perm']['launches'][0]}), "
+                                                  f"{pmc['k_rs_code_perm']['source']}" if "k_rs_code_perm" in pmc else None),
                                  "kernel": "k_rs_code_perm",
                                  "work": f"{inst} x ({k} L read + {m} L written), L = {L}"}}
     sub = {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} instances of a 1 MiB proposal (shard {L} B)",

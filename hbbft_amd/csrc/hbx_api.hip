@@ -1129,8 +1129,11 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
   if (!c->coin_sig.ensure(m * sizeof(g2a)) || !c->coin_sig_st.ensure(m * 4) || !c->coin_valid.ensure(m))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
   if (c->coin_ready_ev) HIPCHK(c, hipStreamWaitEvent(s, c->coin_ready_ev, 0));  // the nonces' hashes are in
-  hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, d_sig96, m, c->coin_sig.as<g2a>(),
-                     c->coin_sig_st.as<int32_t>());
+  {
+    timed t_(c, HBX_K_DECODE_SIGS, s);
+    hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, d_sig96, m, c->coin_sig.as<g2a>(),
+                       c->coin_sig_st.as<int32_t>());
+  }
   HIPCHK(c, hipGetLastError());
   // two lanes per check when one lane per check would leave SIMDs idle (a coin round of 256
   // instances at N = 128 is 512 one-lane waves on 1,024 SIMDs), or when asked for

@@ -99,7 +99,8 @@ CT_UNDECODABLE = 3
 
 # kernel ids of hbx_kernel_time (include/hbx.h)
 KERNELS = {"prepare_ct": 0, "prepare_lines": 1, "ct_checks": 2, "verify_shares": 3, "combine": 4,
-           "verify_sig": 5, "combine_sigs": 6, "rs_code": 7, "merkle_leaves": 8, "hash_nonces": 9}
+           "verify_sig": 5, "combine_sigs": 6, "rs_code": 7, "merkle_leaves": 8, "hash_nonces": 9,
+           "decode_sigs": 10}
 
 _lib = None
 

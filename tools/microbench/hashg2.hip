@@ -16,7 +16,7 @@ __global__ void __launch_bounds__(64) k_hash(const uint8_t* digests, uint32_t co
   if (j >= count) return;
   HBX_PHASE(0);
   g2j h;
-  if (hash_g2_group<16>(digests + 32 * j, true, h)) {
+  if (hash_g2_group<16>(digests + 32 * j, true, h, false)) {  // stops at h_eff P, as k_prepare_ct does
     const g2a a = g2_to_affine(h);
     out[j] = a;
   }
