@@ -1131,8 +1131,9 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
   if (c->coin_ready_ev) HIPCHK(c, hipStreamWaitEvent(s, c->coin_ready_ev, 0));  // the nonces' hashes are in
   {
     timed t_(c, HBX_K_DECODE_SIGS, s);
+    // curve membership only: the share checks test G2 membership on their Miller loop's [|x|] sigma
     hipLaunchKernelGGL(k_decompress_g2, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, d_sig96, m, c->coin_sig.as<g2a>(),
-                       c->coin_sig_st.as<int32_t>());
+                       c->coin_sig_st.as<int32_t>(), 0u);
   }
   HIPCHK(c, hipGetLastError());
   // two lanes per check when one lane per check would leave SIMDs idle (a coin round of 256
@@ -1250,7 +1251,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
                      c->vs_blob.as<uint8_t>(), c->vs_off.as<uint64_t>(), count, c->vs_H.as<g2a>(), c->digest, 1);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_decompress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_sig96.as<uint8_t>(), (size_t)count,
-                     c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>());
+                     c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(), 1u);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
                      c->vs_lines.as<line_pre>(), c->vs_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,

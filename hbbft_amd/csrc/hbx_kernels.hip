@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   if (i >= n) return;  // whole pairs
   const size_t idx = (size_t)inst * n + i;
   const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
-  bool v = false;
+  bool v = false, tf = true;
   if (res == HBX_SHARE_VALID) {
     // lane 0: e(pk_i, H'); lane 1: e(-[m] g1, sigma_i)  (H' = [m] H: the same verdict)
     g2a Q = l1 ? sig[idx] : H[inst];
@@ -699,8 +699,11 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
     }
     const bool use = !(Q.inf || P.inf);  // a pairing with the identity contributes 1
     const fqd z = fqd_zero();
+    g2jd T;
     const fq12d f = miller_loop_mixed_d(nullptr, z, z, false, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(P.x),
-                                        fqd_from_fq(P.y), use);
+                                        fqd_from_fq(P.y), use, &T);
+    // sigma's membership in G2 from lane 1's T = [|x|] sigma (decode skipped it); lane 0's is H's
+    tf = !l1 || g2_torsion_free_from_T(T, Q);
     lds_u32* reg = (lds_u32*)region;
     const int pl = lane & ~1;
     const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
@@ -715,7 +718,15 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
     HBX_SEQ();
     v = final_exp2d_is_one(A, B, G1, G2, l1);
   }
-  if (!l1) valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+  // lane 1's membership bit to lane 0 (the pair is active or inactive together).  The exchange runs
+  // on every lane before the bits are combined: inside `tf && ...` lane 1 (tf false) would skip it
+  // and lane 0 would read lane 1's unwritten operand register.
+  const int tf_other = __shfl_xor((int)tf, 1);
+  const bool tf_pair = tf && tf_other != 0;
+  if (!l1) {
+    if (res == HBX_SHARE_VALID && !tf_pair) valid[idx] = HBX_SHARE_UNDECODABLE;
+    else valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
+  }
 }
 #endif
 
@@ -1415,8 +1426,11 @@ __global__ void __launch_bounds__(64) k_h2_from_heff(const g2a* __restrict__ Hp,
   H[j] = Hp[j].inf ? Hp[j] : g2_to_affine(g2_heff_to_h2(g2_from_affine(Hp[j])));
 }
 
+// subgroup = 0: curve membership only -- the coin's share checks (k_verify_sig_shares[2]) take G2
+// membership from their Miller loop's [|x|] sigma and report HBX_SHARE_UNDECODABLE themselves.
 __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict__ comp, size_t count,
-                                                      g2a* __restrict__ out, int32_t* __restrict__ status) {
+                                                      g2a* __restrict__ out, int32_t* __restrict__ status,
+                                                      uint32_t subgroup) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   g2a p;
@@ -1424,7 +1438,7 @@ __global__ void __launch_bounds__(64) k_decompress_g2(const uint8_t* __restrict_
   // G2.  A share sig_i + T (T of cofactor order) could otherwise pass the ate check and carry T
   // into the combined signature and its parity bit.
   int32_t st = g2_decompress(comp + i * 96, p);
-  if (st == HBX_PT_OK && !g2_is_torsion_free(p)) st = HBX_PT_NOT_IN_SUBGROUP;
+  if (subgroup && st == HBX_PT_OK && !g2_is_torsion_free(p)) st = HBX_PT_NOT_IN_SUBGROUP;
   status[i] = st;
   out[i] = p;
 }
@@ -1465,15 +1479,26 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares(const line_pre_d* __re
   const uint32_t inst = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)inst * n + i;
-  const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
+  uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
   bool v = false;
   if (res == HBX_SHARE_VALID) {
     g1a ng;  // -[m] g1 against H' = [m] H
     ng.x = fq_from_const(G1_MGEN_X);
     ng.y = fq_neg(fq_from_const(G1_MGEN_Y));
     ng.inf = false;
-    v = check_mixed_d(lines + (size_t)inst * MILLER_LINES, pk[i], H[inst].inf, sig[idx], ng,
-                      (lds_u32*)(gslots + threadIdx.x));
+    // check_mixed_d with sigma's membership in G2 from the loop's final T (decode skipped it)
+    const g1a PA = pk[i];
+    const g2a QB = sig[idx];
+    const bool skipA = PA.inf || H[inst].inf, skipB = QB.inf;
+    g2jd T;
+    const fq12d f = miller_loop_mixed_d(lines + (size_t)inst * MILLER_LINES, fqd_from_fq(PA.x), fqd_from_fq(PA.y), !skipA,
+                                        fq2d_from_fq2(QB.x), fq2d_from_fq2(QB.y), fqd_from_fq(ng.x), fqd_from_fq(ng.y),
+                                        !skipB, &T);
+    if (!skipB && !g2_torsion_free_from_T(T, QB)) {
+      res = HBX_SHARE_UNDECODABLE;
+    } else {
+      v = (skipA && skipB) || fq12d_is_one(final_exponentiation_d(f, (lds_u32*)(gslots + threadIdx.x)));
+    }
   }
   valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
 }

@@ -98,9 +98,11 @@ HBX_HDNI fq12d fq12d_mul_by_014_f2(const fq12d& f, const fq2d& c0, const fq2d& c
 }
 // pairing.hpp miller_loop_mixed: pair A over prepared digit-form lines (plain loads: the lines may
 // differ per lane), pair B's lines generated from QB = (qx, qy) and evaluated un-normalised at PB.
-// One out-of-line copy (the coin and the PublicKey::verify kernels share it).
+// One out-of-line copy (the coin and the PublicKey::verify kernels share it).  With `Tout`, the
+// loop's final T = [|x|] QB (Jacobian) is stored there: the coin checks take QB's G2 membership
+// from it (g2_torsion_free_from_T) instead of a separate [x] multiplication at decode.
 HBX_HDNI fq12d miller_loop_mixed_d(const line_pre_d* LA, const fqd& ax, const fqd& ay, bool useA, const fq2d& qx,
-                                 const fq2d& qy, const fqd& bx, const fqd& by, bool useB) {
+                                 const fq2d& qy, const fqd& bx, const fqd& by, bool useB, g2jd* Tout = nullptr) {
   fq12d f = fq12d_one();
   g2jd T{qx, qy, fq2d{fqd_const(FQD_ONE), fqd_zero()}};
   int k = 0;
@@ -122,7 +124,18 @@ HBX_HDNI fq12d miller_loop_mixed_d(const line_pre_d* LA, const fqd& ax, const fq
       k++;
     }
   }
+  if (Tout) *Tout = T;
   return fq12d_conj(f);
+}
+
+// Q in G2 from the mixed Miller loop's final T = [|x|] Q (eprint 2021/1130 sec. 4: psi(Q) == [x] Q,
+// x = -|x|; curve.hpp g2_is_torsion_free computes the same multiplication by itself).  An
+// exceptional addition on the way ([k] Q = +-Q, only for Q of small order) leaves T at Z = 0,
+// which never equals the finite -psi(Q): rejected, as Q is not in G2.
+HBX_HD bool g2_torsion_free_from_T(const g2jd& T, const g2a& Q) {
+  if (Q.inf) return true;
+  const g2j t{fq2d_to_fq2(T.x), fq2d_to_fq2(T.y), fq2d_to_fq2(T.z)};
+  return g2j_eq(g2_neg(t), g2_psi(g2_from_affine(Q)));
 }
 
 // Out-of-line copies (one each) for the final exponentiation's cold calls.

@@ -366,3 +366,39 @@ def test_subgroup_checks_match_order_r(hc):
     small = bls.g1_mul(_rand_curve_point_g1(rnd), bls.R)  # order divides h1
     mixed = bls.g1_add(small, bls.g1_mul(bls.G1_GEN, 9))
     assert hc.hc_g1_torsion_free(_be(mixed[0]), _be(mixed[1])) == 0
+
+
+def test_g2_membership_from_miller_T(hc):
+    """The coin share checks take sigma's membership in G2 from their Miller loop's final
+    T = [|x|] sigma (hbx_kernels.hip k_verify_sig_shares[2]); it must agree with the decode-time
+    check (g2_is_torsion_free) on subgroup points, on points of E'(Fq2) outside G2, and on every
+    decodable share of the coin fixtures (incl. their cofactor-torsion shares)."""
+    import numpy as np
+
+    hc.hc_g2_membership.argtypes = [ctypes.c_char_p]
+    rnd = random.Random(5)
+    seen = {0: 0, 3: 0}
+    for _ in range(3):
+        q = bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R))
+        r = hc.hc_g2_membership(bls.g2_compress(q))
+        assert r == 3
+        seen[3] += 1
+    k = 1
+    while seen[0] < 3:  # points of the twist that are not cofactor-cleared: almost surely outside G2
+        k += 1
+        x = (k, 1)
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is None:
+            continue
+        r = hc.hc_g2_membership(bls.g2_compress((x, y)))
+        assert r in (0, 3)
+        seen[r] += 1
+    for name in ("coin_n7", "coin_n128"):
+        d = np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"), allow_pickle=False)
+        sigs = d["sigs"].reshape(-1, 96)
+        for s in sigs[:: max(1, len(sigs) // 400)]:
+            r = hc.hc_g2_membership(s.tobytes())
+            assert r in (-1, 0, 3), r
+        st = d["expect_share_status"].reshape(-1)
+        for s in sigs[st == 3]:  # UNDECODABLE shares: bad bytes or torsion; both checks reject alike
+            assert hc.hc_g2_membership(s.tobytes()) in (-1, 0)

@@ -300,3 +300,19 @@ int hc_hash_g2_digest(const uint8_t* d32, uint8_t* out96) {
   g2_compress(g2_to_affine(hash_g2_from_digest(d32)), out96); return 0;
 }
 }
+extern "C" {
+// G2 membership of a compressed point two ways: bit 0 from the mixed Miller loop's final
+// T = [|x|] Q (g2_torsion_free_from_T, the coin checks), bit 1 from g2_is_torsion_free (decode);
+// -1 if the bytes do not decode to a curve point.
+int hc_g2_membership(const uint8_t* q96) {
+  g2a Q;
+  const int32_t st = g2_decompress(q96, Q);
+  if (st != HBX_PT_OK && st != HBX_PT_INFINITY) return -1;
+  const fqd z = fqd_zero();
+  const fq gx = fq_from_const(G1_MGEN_X), gy = fq_neg(fq_from_const(G1_MGEN_Y));
+  g2jd T;
+  (void)miller_loop_mixed_d(nullptr, z, z, false, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(gx), fqd_from_fq(gy),
+                            !Q.inf, &T);
+  return (g2_torsion_free_from_T(T, Q) ? 1 : 0) | (g2_is_torsion_free(Q) ? 2 : 0);
+}
+}
