@@ -389,6 +389,31 @@ HBX_HDNI g2j g2_mul_u64_naf(const g2a& P, uint64_t k) {
   return acc;
 }
 
+// k P for a 64-bit k and an affine P by 4-bit fixed windows (g1_mul_u64_w4's schedule in G2): a
+// table (0..15) P in per-lane scratch, then 15 x (4 doublings + 1 addition).  Every lane adds its
+// own table entry once per window, so a wave of lanes with different scalars issues 15 additions
+// -- g2_mul_u64_naf's addition site is taken whenever ANY lane has a nonzero digit (~66 additions
+// per wave): k_combine_sigs' 64-bit multiplications 5.3 -> ~3.5 ms at one wave per SIMD
+// (tools/microbench/combsig.hip).
+HBX_HDNI g2j g2_mul_u64_w4(const g2a& P, uint64_t k) {
+  g2j tab[16];
+  tab[0] = g2_identity();
+  tab[1] = g2_from_affine(P);
+#pragma unroll 1
+  for (int i = 2; i < 16; i++) tab[i] = g2_add_mixed(tab[i - 1], P);
+  g2j acc = tab[k >> 60];
+  g2j nxt = tab[(k >> 56) & 0xFu];
+#pragma unroll 1
+  for (int w = 14; w >= 0; w--) {
+    const g2j cur = nxt;
+    if (w > 0) nxt = tab[(k >> (4 * (w - 1))) & 0xFu];
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) acc = g2_dbl(acc);
+    acc = g2_add(acc, cur);
+  }
+  return acc;
+}
+
 HBX_HDNI g2a g2_to_affine(const g2j& p) {
   g2a r;
   if (g2j_is_identity(p)) {

@@ -1580,7 +1580,8 @@ __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
 // lambda_k = d0 + d1 X + d2 X^2 + d3 X^3 (|d_i| < X < 2^64),
 //     lambda_k S_k = d0 S_k - d1 psi(S_k) + d2 psi^2(S_k) - d3 psi^3(S_k),
 // four independent 64-bit scalar multiplications, one per lane (lane 4k + i), instead of one
-// 255-bit multiplication: a quarter of the doubling chain.
+// 255-bit multiplication: a quarter of the doubling chain; 4-bit fixed windows (g2_mul_u64_w4), so
+// the lanes' different digits do not serialise the additions.
 //
 // B3 master check (PublicKey::verify(sig, nonce), common_coin.rs:196) in the same block, on its
 // last wave: every S_k was verified, e(pk_k, H) = e(g1, S_k), so by bilinearity
@@ -1663,7 +1664,7 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
       g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
       for (int e = 0; e < i; e++) P = g2_psi(P);  // affine in, affine out (Z = 1)
       g2a Pa{P.x, i & 1 ? fq2_neg(P.y) : P.y, false};
-      if (d[i] != 0) acc2 = g2_add(acc2, g2_mul_u64_naf(Pa, d[i]));
+      if (d[i] != 0) acc2 = g2_add(acc2, g2_mul_u64_w4(Pa, d[i]));
     }
 #pragma unroll 1
     for (int m = 1; m < 64; m <<= 1) acc2 = g2_add(acc2, g2j_shfl_xor(acc2, m));

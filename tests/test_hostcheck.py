@@ -402,3 +402,12 @@ def test_g2_membership_from_miller_T(hc):
         st = d["expect_share_status"].reshape(-1)
         for s in sigs[st == 3]:  # UNDECODABLE shares: bad bytes or torsion; both checks reject alike
             assert hc.hc_g2_membership(s.tobytes()) in (-1, 0)
+
+
+def test_g2_mul_u64_windows_match_naf(hc):
+    """k_combine_sigs' 64-bit G2 multiplications by 4-bit windows equal the NAF ladder's."""
+    hc.hc_g2_mul_u64_cmp.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    rnd = random.Random(9)
+    q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+    for k in [1, 2, 15, 16, 17, 0xFFFFFFFFFFFFFFFF, 0xd201000000010000] + [rnd.getrandbits(64) for _ in range(6)]:
+        assert hc.hc_g2_mul_u64_cmp(q, k) == 1, hex(k)

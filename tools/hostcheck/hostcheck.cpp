@@ -316,3 +316,14 @@ int hc_g2_membership(const uint8_t* q96) {
   return (g2_torsion_free_from_T(T, Q) ? 1 : 0) | (g2_is_torsion_free(Q) ? 2 : 0);
 }
 }
+extern "C" {
+// [k] Q (Q compressed, k 64-bit) by g2_mul_u64_w4 and by g2_mul_u64_naf: 1 if the affine results
+// agree, 0 if not, -1 if Q does not decode.
+int hc_g2_mul_u64_cmp(const uint8_t* q96, uint64_t k) {
+  g2a Q;
+  if (g2_decompress(q96, Q) != HBX_PT_OK) return -1;
+  const g2a a = g2_to_affine(g2_mul_u64_w4(Q, k)), b = g2_to_affine(g2_mul_u64_naf(Q, k));
+  if (a.inf || b.inf) return a.inf == b.inf ? 1 : 0;
+  return fq2_eq(a.x, b.x) && fq2_eq(a.y, b.y) ? 1 : 0;
+}
+}
