@@ -40,5 +40,14 @@ int main() {
   const char* names[6] = {"start", "drawn", "residuosity exp", "sqrt from norm", "cofactor clearing", "to_affine+store"};
   for (int k = 1; k < 6; k++) printf("%-20s %8.3f ms\n", names[k], (st[k] - st[k - 1]) / 100e3);
   printf("total                %8.3f ms\n", (st[5] - st[0]) / 100e3);
+  // checksum of the affine results (builds with -DHBX_G2_GROUP_DIGITS=0/1 must agree)
+  g2a* ho = new g2a[count];
+  if (hipMemcpy(ho, o, count * sizeof(g2a), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  uint64_t sum = 0;
+  for (uint32_t j = 0; j < count; j++) {
+    const fq x = fq_canon(ho[j].x.c0), y = fq_canon(ho[j].y.c1);
+    for (int q = 0; q < 12; q++) sum = sum * 1000003u + x.l[q] + 7u * y.l[q];
+  }
+  printf("checksum             %016llx\n", (unsigned long long)sum);
   return 0;
 }
