@@ -1165,6 +1165,9 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
       hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_Hp.as<g2a>(),
                          c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(), d_present, n,
                          c->coin_valid.as<uint8_t>(), c->gslot.as<uint32_t>());
+      HIPCHK(c, hipGetLastError());
+      hipLaunchKernelGGL(k_verify_sig_shares2_fe, dim3((n + 31) / 32, count), dim3(64), 0, s, n,
+                         c->coin_valid.as<uint8_t>(), c->gslot.as<uint32_t>());
     } else {
       hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
                          c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),

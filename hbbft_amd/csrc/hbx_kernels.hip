@@ -672,6 +672,10 @@ __global__ void __launch_bounds__(64) k_verify_shares2(const g1a* __restrict__ S
 // one-lane check's (one pair's lines, the squarings on both lanes), and 32,768 checks fill 1,024
 // waves instead of 512.  Same verdicts as k_verify_sig_shares (common_coin.rs:151).
 #if HBX_IN_TU(7)
+// Split in two kernels, each register-allocated on its own: k_verify_sig_shares2 runs the pair's
+// Miller loops (sigma's membership in G2 from lane 1's T) and the pair product, and leaves the
+// product's halves in the pair's global slot G1 with status SHARE_PENDING; k_verify_sig_shares2_fe
+// runs the two-lane final exponentiation of the pending pairs.  Same grid for both.
 __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict__ H, const g1a* __restrict__ pk,
                                                            uint32_t n_keys, const g2a* __restrict__ sig,
                                                            const int32_t* __restrict__ sig_status,
@@ -685,7 +689,7 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   if (i >= n) return;  // whole pairs
   const size_t idx = (size_t)inst * n + i;
   const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
-  bool v = false, tf = true;
+  bool tf = true;
   if (res == HBX_SHARE_VALID) {
     // lane 0: e(pk_i, H'); lane 1: e(-[m] g1, sigma_i)  (H' = [m] H: the same verdict)
     g2a Q = l1 ? sig[idx] : H[inst];
@@ -698,17 +702,15 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
       P = pk[i];
     }
     const bool use = !(Q.inf || P.inf);  // a pairing with the identity contributes 1
-    const fqd z = fqd_zero();
-    g2jd T;
-    const fq12d f = miller_loop_mixed_d(nullptr, z, z, false, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(P.x),
-                                        fqd_from_fq(P.y), use, &T);
+    g2jd T{};
+    const fq12d f = use ? miller_loop_gen_parked_d(fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(P.x),
+                                                   fqd_from_fq(P.y), (lds_u32*)region + lane, T)
+                        : fq12d_one();
     // sigma's membership in G2 from lane 1's T = [|x|] sigma (decode skipped it); lane 0's is H's
     tf = !l1 || g2_torsion_free_from_T(T, Q);
     lds_u32* reg = (lds_u32*)region;
     const int pl = lane & ~1;
     const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
-    uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
-    const slot2<uint32_t*> G1{gb, 64u}, G2{gb + LDS_FQ6D_PACKED * 64, 64u};
     // each lane parks its whole Fq12 in its slot (A: f_A, B: f_B), both halves
     const slot2<lds_u32*>& mine = l1 ? B : A;
     slot_put_fq6d(mine.half(0), mine.stride, fq6d_reduce(f.c0));
@@ -716,17 +718,38 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
     HBX_SEQ();
     op_mul(B, A, false, false, l1);  // B = f_B f_A, lane k its half
     HBX_SEQ();
-    v = final_exp2d_is_one(A, B, G1, G2, l1);
+    uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
+    const int h = l1 ? 1 : 0;
+#pragma unroll 6
+    for (int k = 0; k < LDS_FQ6D_PACKED; k++) gb[h + k * 64] = B.half(h)[k * 64];
   }
   // lane 1's membership bit to lane 0 (the pair is active or inactive together).  The exchange runs
   // on every lane before the bits are combined: inside `tf && ...` lane 1 (tf false) would skip it
   // and lane 0 would read lane 1's unwritten operand register.
   const int tf_other = __shfl_xor((int)tf, 1);
   const bool tf_pair = tf && tf_other != 0;
-  if (!l1) {
-    if (res == HBX_SHARE_VALID && !tf_pair) valid[idx] = HBX_SHARE_UNDECODABLE;
-    else valid[idx] = res == HBX_SHARE_VALID ? (v ? HBX_SHARE_VALID : HBX_SHARE_INVALID) : res;
-  }
+  if (!l1) valid[idx] = res != HBX_SHARE_VALID ? res : tf_pair ? SHARE_PENDING : (uint8_t)HBX_SHARE_UNDECODABLE;
+}
+__global__ void __launch_bounds__(64) k_verify_sig_shares2_fe(uint32_t n, uint8_t* __restrict__ valid,
+                                                              uint32_t* __restrict__ gslot) {
+  __shared__ uint32_t region[LDS2_DWORDS * 64];
+  const int lane = (int)(threadIdx.x & 63);
+  const bool l1 = (lane & 1) != 0;
+  const uint32_t i = blockIdx.x * 32 + (uint32_t)(lane >> 1);
+  if (i >= n) return;
+  const size_t idx = (size_t)blockIdx.y * n + i;
+  if (valid[idx] != SHARE_PENDING) return;  // pair-uniform
+  lds_u32* reg = (lds_u32*)region;
+  const int pl = lane & ~1;
+  const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
+  uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
+  const slot2<uint32_t*> G1{gb, 64u}, G2{gb + LDS_FQ6D_PACKED * 64, 64u};
+  const int h = l1 ? 1 : 0;
+#pragma unroll 6
+  for (int k = 0; k < LDS_FQ6D_PACKED; k++) B.half(h)[k * 64] = gb[h + k * 64];
+  HBX_SEQ();
+  const bool v = final_exp2d_is_one(A, B, G1, G2, l1);
+  if (!l1) valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
 }
 #endif
 

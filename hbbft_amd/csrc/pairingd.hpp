@@ -49,7 +49,7 @@ struct g2jd {
 };
 // Raw line through the doubling of T, scaled by 2 Y Z^3: c0 = 3X^3 - 2Y^2, c1 = -3X^2 Z^2,
 // c2 = 2YZ^3;  T <- 2T.
-HBX_HDNI void line_dbl_step_d(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
+HBX_HD void line_dbl_step_di(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
   const fq2d A = fq2d_sqr(T.x);
   const fq2d B = fq2d_sqr(T.y);
   const fq2d C = fq2d_sqr(B);
@@ -66,6 +66,7 @@ HBX_HDNI void line_dbl_step_d(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
   c2 = fq2d_mul(Z3, ZZ);
   T = g2jd{X3, Y3, Z3};
 }
+HBX_HDNI void line_dbl_step_d(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) { line_dbl_step_di(T, c0, c1, c2); }
 // Raw line through T and the affine base point (qx, qy), scaled by den = Z (X - xQ Z^2):
 // c0 = num xQ - yQ den, c1 = -num, c2 = den;  T <- T + Q (madd-2007-bl).
 HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
@@ -89,12 +90,15 @@ HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0,
   T = g2jd{X3, Y3, Z3};
 }
 // f * (c0 + c1 v + c4 v w) with c4 in Fq2 (an un-normalised line at a G1 point)
-HBX_HDNI fq12d fq12d_mul_by_014_f2(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
+HBX_HD fq12d fq12d_mul_by_014_f2_i(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
   const fq6d aa = fq6d_mul_by_01(f.c0, c0, c1);
   const fq6d bb = fq6d{fq2d_mul_xi(fq2d_mul(f.c1.c2, c4)), fq2d_mul(f.c1.c0, c4), fq2d_mul(f.c1.c1, c4)};
   const fq2d o = fq2d_norm(fq2d_add(c1, c4));
   const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, o);
   return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bb), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bb))};
+}
+HBX_HDNI fq12d fq12d_mul_by_014_f2(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
+  return fq12d_mul_by_014_f2_i(f, c0, c1, c4);
 }
 // pairing.hpp miller_loop_mixed: pair A over prepared digit-form lines (plain loads: the lines may
 // differ per lane), pair B's lines generated from QB = (qx, qy) and evaluated un-normalised at PB.
@@ -125,6 +129,29 @@ HBX_HDNI fq12d miller_loop_mixed_d(const line_pre_d* LA, const fqd& ax, const fq
     }
   }
   if (Tout) *Tout = T;
+  return fq12d_conj(f);
+}
+
+// One pair with its lines generated from (qx, qy) and evaluated at (bx, by) -- miller_loop_mixed_d
+// with pair A off -- the doubling steps and line products inlined (the two-lane coin check's
+// per-lane loop: the out-of-line steps passed the Fq12 accumulator through the call frames, 11.5
+// -> 9.3 ms per 1,024-wave launch, tools/microbench/coin_parts.hip).  T = [|x|] Q on return.
+HBX_HD fq12d miller_loop_gen_d(const fq2d& qx, const fq2d& qy, const fqd& bx, const fqd& by, g2jd& T) {
+  fq12d f = fq12d_one();
+  T = g2jd{qx, qy, fq2d{fqd_const(FQD_ONE), fqd_zero()}};
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12d_sqr(f);
+#pragma unroll 1
+    for (int s = 0; s < (((BLS_X >> i) & 1) ? 2 : 1); s++) {
+      fq2d c0, c1, c2;
+      if (s == 0) line_dbl_step_di(T, c0, c1, c2);
+      else line_add_step_d(T, qx, qy, c0, c1, c2);
+      HBX_SEQ();
+      f = fq12d_mul_by_014_f2_i(f, c0, fq2d_mul_fq(c1, bx), fq2d_mul_fq(c2, by));
+      HBX_SEQ();
+    }
+  }
   return fq12d_conj(f);
 }
 
@@ -188,6 +215,42 @@ HBX_HD fq12d miller_loop2_parked_d(const line_pre_d* LA, bool useA, const line_p
         f = fq12d_mul_by_014(f, L.c0, fq2d_mul_fq(L.c1, px), py);
       }
       if (b) k++;
+    }
+  }
+  return fq12d_conj(f);
+}
+
+// miller_loop_gen_d with (qx, qy, bx, by) parked in this lane's LDS slot (free until the final
+// exponentiation): 84 registers fewer across the loop; the add steps and every line evaluation
+// read them back.  Same element, same T.  (Parking T as well, Q re-read from memory at the add
+// steps, spilled more: 748 VGPRs, 18.3 ms per coin round's checks against 367 and 16.3 ms.)
+HBX_HD fq12d miller_loop_gen_parked_d(const fq2d& qx, const fq2d& qy, const fqd& bx, const fqd& by, lds_u32* park,
+                                      g2jd& T) {
+  park_put_fqd(park, 0, qx.c0);
+  park_put_fqd(park, 1, qx.c1);
+  park_put_fqd(park, 2, qy.c0);
+  park_put_fqd(park, 3, qy.c1);
+  park_put_fqd(park, 4, bx);
+  park_put_fqd(park, 5, by);
+  fq12d f = fq12d_one();
+  T = g2jd{qx, qy, fq2d{fqd_const(FQD_ONE), fqd_zero()}};
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12d_sqr(f);
+#pragma unroll 1
+    for (int s = 0; s < (((BLS_X >> i) & 1) ? 2 : 1); s++) {
+      fq2d c0, c1, c2;
+      HBX_SEQ();
+      if (s == 0) {
+        line_dbl_step_di(T, c0, c1, c2);
+      } else {
+        const fq2d px{park_get_fqd(park, 0), park_get_fqd(park, 1)}, py{park_get_fqd(park, 2), park_get_fqd(park, 3)};
+        line_add_step_d(T, px, py, c0, c1, c2);
+      }
+      HBX_SEQ();
+      const fqd ex = park_get_fqd(park, 4), ey = park_get_fqd(park, 5);
+      f = fq12d_mul_by_014_f2_i(f, c0, fq2d_mul_fq(c1, ex), fq2d_mul_fq(c2, ey));
+      HBX_SEQ();
     }
   }
   return fq12d_conj(f);

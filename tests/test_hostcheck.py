@@ -411,3 +411,13 @@ def test_g2_mul_u64_windows_match_naf(hc):
     q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
     for k in [1, 2, 15, 16, 17, 0xFFFFFFFFFFFFFFFF, 0xd201000000010000] + [rnd.getrandbits(64) for _ in range(6)]:
         assert hc.hc_g2_mul_u64_cmp(q, k) == 1, hex(k)
+
+
+def test_miller_gen_matches_mixed(hc):
+    """The two-lane coin check's inlined one-pair loop equals the mixed loop with pair A off."""
+    hc.hc_miller_gen_cmp.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    rnd = random.Random(17)
+    for _ in range(3):
+        q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+        assert hc.hc_miller_gen_cmp(q, 0) == 1
+        assert hc.hc_miller_gen_cmp(q, 1) == 1  # (qx, qy, bx, by) parked in the lane's slot

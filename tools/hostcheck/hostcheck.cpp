@@ -327,3 +327,24 @@ int hc_g2_mul_u64_cmp(const uint8_t* q96, uint64_t k) {
   return fq2_eq(a.x, b.x) && fq2_eq(a.y, b.y) ? 1 : 0;
 }
 }
+extern "C" {
+// miller_loop_gen_d (inlined steps, two-lane coin check) against miller_loop_mixed_d with pair A
+// off: the same Fq12 element and the same final T.  1 if both agree.
+int hc_miller_gen_cmp(const uint8_t* q96, int parked) {
+  g2a Q;
+  if (g2_decompress(q96, Q) != HBX_PT_OK) return -1;
+  const fqd z = fqd_zero();
+  const fqd bx = fqd_from_fq(fq_from_const(G1_MGEN_X)), by = fqd_from_fq(fq_neg(fq_from_const(G1_MGEN_Y)));
+  g2jd T1, T2;
+  const fq12d f1 = miller_loop_mixed_d(nullptr, z, z, false, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), bx, by, true, &T1);
+  uint32_t park[6 * 14];
+  const fq12d f2 = parked ? miller_loop_gen_parked_d(fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), bx, by, park, T2)
+                          : miller_loop_gen_d(fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), bx, by, T2);
+  const fqd* a = &f1.c0.c0.c0;
+  const fqd* b = &f2.c0.c0.c0;
+  for (int q = 0; q < 12; q++)
+    if (!fq_eq(fq_canon(fqd_to_fq(a[q])), fq_canon(fqd_to_fq(b[q])))) return 0;
+  const g2j t1{fq2d_to_fq2(T1.x), fq2d_to_fq2(T1.y), fq2d_to_fq2(T1.z)}, t2{fq2d_to_fq2(T2.x), fq2d_to_fq2(T2.y), fq2d_to_fq2(T2.z)};
+  return g2j_eq(t1, t2) ? 1 : 0;
+}
+}

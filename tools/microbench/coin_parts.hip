@@ -59,6 +59,57 @@ __global__ void __launch_bounds__(64) k_coin2(uint32_t* out, uint32_t* gslot) {
   out[s] = v ? 1u : 0u;
 }
 
+// the per-lane Miller loop of k_coin2<false> with every step inlined (the shipped loop calls
+// out-of-line line steps and sparse products, passing the Fq12 accumulator through its frame)
+__device__ __forceinline__ void dbl_i(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
+  const fq2d A = fq2d_sqr(T.x);
+  const fq2d B = fq2d_sqr(T.y);
+  const fq2d C = fq2d_sqr(B);
+  const fq2d ZZ = fq2d_sqr(T.z);
+  const fq2d E = fq2d_norm(fq2d_add(fq2d_dbl(A), A));
+  c0 = fq2d_reduce(fq2d_sub(fq2d_mul(E, T.x), fq2d_dbl(B)));
+  c1 = fq2d_neg(fq2d_mul(E, ZZ));
+  const fq2d D = fq2d_reduce(fq2d_dbl(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(T.x, B)), A), C)));
+  const fq2d F = fq2d_sqr(E);
+  const fq2d X3 = fq2d_reduce(fq2d_sub(F, fq2d_dbl(D)));
+  const fq2d C8 = fq2d_dbl(fq2d_reduce(fq2d_dbl(fq2d_dbl(C))));
+  const fq2d Y3 = fq2d_reduce(fq2d_sub(fq2d_mul(E, fq2d_sub(D, X3)), C8));
+  const fq2d Z3 = fq2d_reduce(fq2d_dbl(fq2d_mul(T.y, T.z)));
+  c2 = fq2d_mul(Z3, ZZ);
+  T = g2jd{X3, Y3, Z3};
+}
+__device__ __forceinline__ fq12d mul014_i(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
+  const fq6d aa = fq6d_mul_by_01(f.c0, c0, c1);
+  const fq6d bb = fq6d{fq2d_mul_xi(fq2d_mul(f.c1.c2, c4)), fq2d_mul(f.c1.c0, c4), fq2d_mul(f.c1.c1, c4)};
+  const fq2d o = fq2d_norm(fq2d_add(c1, c4));
+  const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, o);
+  return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bb), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bb))};
+}
+__global__ void __launch_bounds__(64) k_coin2_inl(uint32_t* out) {
+  const int lane = (int)(threadIdx.x & 63);
+  const uint32_t s = blockIdx.x * 64 + lane;
+  const fq2d qx{seed_fqd(s), seed_fqd(s + 1)}, qy{seed_fqd(s + 2), seed_fqd(s + 3)};
+  const fqd bx = seed_fqd(s + 5), by = seed_fqd(s + 6);
+  fq12d f = fq12d_one();
+  g2jd T{qx, qy, fq2d{fqd_const(FQD_ONE), fqd_zero()}};
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12d_sqr(f);
+#pragma unroll 1
+    for (int st = 0; st < (((BLS_X >> i) & 1) ? 2 : 1); st++) {
+      fq2d c0, c1, c2;
+      if (st == 0) dbl_i(T, c0, c1, c2);
+      else line_add_step_d(T, qx, qy, c0, c1, c2);
+      HBX_SEQ();
+      f = mul014_i(f, c0, fq2d_mul_fq(c1, bx), fq2d_mul_fq(c2, by));
+      HBX_SEQ();
+    }
+  }
+  uint32_t acc = 0;
+  for (int i = 0; i < 14; i++) acc ^= (uint32_t)f.c0.c0.c0.d[i] ^ (uint32_t)f.c1.c2.c1.d[i];
+  out[s] = acc;
+}
+
 // one lane per check: prepared H lines (wave-uniform: one instance per block) + sigma generated
 __global__ void __launch_bounds__(64) k_coin1(const line_pre_d* lines, uint32_t* out) {
   const int lane = (int)(threadIdx.x & 63);
@@ -100,6 +151,7 @@ int main() {
   };
   timeit("K_ml   two-lane Miller only (1024 waves)", [&] { hipLaunchKernelGGL(k_coin2<false>, dim3(blocks2), dim3(64), 0, 0, out, gslot); });
   timeit("K_full two-lane Miller + pair mul + FE2", [&] { hipLaunchKernelGGL(k_coin2<true>, dim3(blocks2), dim3(64), 0, 0, out, gslot); });
+  timeit("K_inl  two-lane Miller, steps inlined", [&] { hipLaunchKernelGGL(k_coin2_inl, dim3(blocks2), dim3(64), 0, 0, out); });
   timeit("K_ml1  one-lane mixed Miller (512 waves)", [&] { hipLaunchKernelGGL(k_coin1, dim3(blocks1), dim3(64), 0, 0, lines, out); });
   CK(hipGetLastError());
   return 0;
