@@ -68,8 +68,9 @@ namespace hbx {
 // ~0).  Every place that masks a digit passes it through an empty asm with the digit as an in/out
 // VGPR operand, which hides what is known about its value and emits nothing.  (Laundering the
 // product operands instead forced the Miller loop's wave-uniform line coefficients out of SGPRs
-// into VGPRs: more registers, spills.)
-#if defined(__HIP_DEVICE_COMPILE__)
+// into VGPRs: more registers, spills.)  The six-lane check's unit is built with HBX_NO_LAUNDER
+// (tools/build.py TU_FLAGS): there the laundered digits raised its spills from 8 to 130 VGPRs.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HBX_NO_LAUNDER)
 #define HBX_LAUNDER(x) __asm__("" : "+v"(x))
 #else
 #define HBX_LAUNDER(x) ((void)0)
