@@ -21,7 +21,7 @@ Multi-GPU (``torchrun``), two modes:
   * ``--scaling strong`` (default; BASELINE config 3): ONE N=256 epoch sharded by proposer column
     (rank g owns proposers [g P/G, (g+1) P/G) with their ciphertexts and share columns; keys are
     replicated); after the combine one RCCL all-gather assembles the per-share status bytes,
-    ciphertext statuses and per-proposer combine statuses.  value = N^2 verifies / epoch time.
+    ciphertext statuses, per-proposer combine statuses and the plaintexts.  value = N^2 verifies / epoch time.
   * ``--scaling weak``: every rank runs one full node-epoch (G epochs in flight, as a node
     pipelining epochs or G co-hosted validators would); no collective on the data path.
     value = G x N^2 verifies / max-over-ranks time.
@@ -96,6 +96,7 @@ def parse(argv=None):
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
+    ap.add_argument("--strong-at-1", action="store_true", help=argparse.SUPPRESS)  # tests: the strong-mode slab path at world 1
     ap.add_argument("--configs", default="C1,C2,C4,C5",
                     help="secondary BASELINE configs in the same line ('' for none); at --gpus > 1 (strong) C4 "
                          "and C5 run sharded by instance")
@@ -190,6 +191,12 @@ def cpu_lib():
 # ----------------------------------------------------------------------------------------------
 # Stack A: HoneyBadger threshold decryption (C2, C3)
 # ----------------------------------------------------------------------------------------------
+def epoch_contributions(n: int, vlen: int):
+    """The N contributions of the synthetic epoch (seeded; every rank can regenerate them)."""
+    rng = np.random.default_rng(0x68626278_00000002)
+    return [rng.integers(0, 256, size=vlen, dtype=np.uint8).tobytes() for _ in range(n)]
+
+
 def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
     """Synthetic inputs of proposers [lo, hi) of one epoch, built on the GPU (hbx producer API)."""
     from hbbft_amd import netinfo
@@ -197,8 +204,7 @@ def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
     sks, sk_shares, master_sk = netinfo.generate_keys(n)
     pk_shares = ctx.public_keys(sk_shares)
     master_pk = ctx.public_keys(master_sk)[0].tobytes()
-    rng = np.random.default_rng(0x68626278_00000002)
-    msgs_all = [rng.integers(0, 256, size=vlen, dtype=np.uint8).tobytes() for _ in range(n)]
+    msgs_all = epoch_contributions(n, vlen)
     r_all = netinfo.scalars_to_be32(netinfo.random_scalars(np.random.default_rng(0x68626278_00000003), n + 1))
     pj = hi - lo
     # own proposers plus one foreign ciphertext (index n) whose shares serve as corruptions
@@ -340,8 +346,11 @@ class EpochBench:
         self.d_out = torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev)
         self.maxv = int(np.max(np.diff(off)))
 
-    def bind_outputs(self, d_valid, d_ct_valid, d_status):
+    def bind_outputs(self, d_valid, d_ct_valid, d_status, d_out=None):
         self.d_valid, self.d_ct_valid, self.d_status = d_valid, d_ct_valid, d_status
+        if d_out is not None:  # the plaintexts straight into the gathered slab
+            assert d_out.numel() >= int(self.off[-1])
+            self.d_out = d_out
 
     def step(self, events=None):
         if events:
@@ -1150,7 +1159,7 @@ def main():
     from hbbft_amd.hbx import Context
 
     n = args.n
-    strong = args.scaling == "strong" and world > 1
+    strong = args.scaling == "strong" and (world > 1 or args.strong_at_1)
     if strong:
         lo, hi = shard.proposer_range(n, world, rank)
     elif args.shard_of > 1 and world == 1:
@@ -1168,10 +1177,14 @@ def main():
     eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share)
     # result slab gathered across ranks: [share status pj*n | ct status pj | combine status pj*4],
     # laid out for the largest column block so every rank's slab has the same size
-    lay = shard.slab_layout(n, shard.max_columns(n, world) if strong else pj)
+    # ... and, at --gpus > 1, the plaintexts (the combined outputs): the rank's decryption blob IS
+    # the slab's plaintext region, sized for the largest rank's proposers
+    pb = shard.max_columns(n, world) * args.vlen if strong else 0
+    lay = shard.slab_layout(n, shard.max_columns(n, world) if strong else pj, pb)
     slab = torch.zeros(lay["size"], dtype=torch.uint8, device=dev)
     eb.bind_outputs(slab[lay["valid"][0]:lay["valid"][0] + pj * n], slab[lay["ct_valid"][0]:lay["ct_valid"][0] + pj],
-                    slab[lay["status"][0]:lay["status"][0] + 4 * pj].view(torch.int32))
+                    slab[lay["status"][0]:lay["status"][0] + 4 * pj].view(torch.int32),
+                    slab[lay["plain"][0]:lay["plain"][1]] if pb else None)
     gathered = [None]
     t = ep["t"]
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
@@ -1208,6 +1221,8 @@ def main():
         full = np.random.default_rng(0x68626278_00000004).integers(0, args.corrupt_every, size=(n, n)) == 0
         full[:, OWN_INDEX] = False
         assert ((gv == 1) == ~full).all() and (gct == 1).all() and (gst == 0).all(), "gathered epoch result"
+        plains = shard.assemble_plaintexts(gathered[0].cpu().numpy(), n, world, [args.vlen] * n, pb)
+        assert plains == epoch_contributions(n, args.vlen), "gathered plaintexts"
 
     ms_epoch_ev = np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)])
     ms_step = elapsed / args.steps * 1e3

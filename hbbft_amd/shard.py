@@ -28,14 +28,23 @@ def max_columns(n: int, world: int) -> int:
     return -(-n // world)
 
 
-def slab_layout(n: int, pj: int):
+def slab_layout(n: int, pj: int, plain_bytes: int = 0):
     """Byte offsets of one rank's result slab for up to ``pj`` proposer columns:
-    share status [pj*n] | ct status [pj] | combine status int32 [pj].  Every rank uses the
-    layout of max_columns(n, world) so the slabs have equal size for one all-gather."""
+    share status [pj*n] | ct status [pj] | combine status int32 [pj] | plaintexts [plain_bytes].
+    The plaintext region is the rank's decryption output blob itself (its proposers' plaintexts
+    back to back at their ciphertexts' V offsets; hbx_decrypt_epoch_d writes it in place), sized
+    for the largest rank's blob.  Every rank uses the layout of max_columns(n, world) so the slabs
+    have equal size for one all-gather."""
     a = pj * n
     b = a + pj
     c = (b + 3) // 4 * 4
-    return {"valid": (0, a), "ct_valid": (a, b), "status": (c, c + 4 * pj), "size": c + 4 * pj}
+    d = c + 4 * pj
+    lay = {"valid": (0, a), "ct_valid": (a, b), "status": (c, d), "size": d}
+    if plain_bytes:
+        e = (d + 7) // 8 * 8
+        lay["plain"] = (e, e + plain_bytes)
+        lay["size"] = (e + plain_bytes + 7) // 8 * 8
+    return lay
 
 
 def all_gather_slabs(slab, world: int):
@@ -54,12 +63,29 @@ def all_gather_slabs(slab, world: int):
     return out.view(world, -1)
 
 
+def assemble_plaintexts(gathered: np.ndarray, n: int, world: int, lens, plain_bytes: int):
+    """Gathered slabs -> every proposer's plaintext (bytes), in proposer order: rank r's blob
+    holds its proposers' plaintexts back to back, lengths ``lens[j]`` (the ciphertexts' |V|,
+    known to every node)."""
+    pm = max_columns(n, world)
+    lay = slab_layout(n, pm, plain_bytes)
+    g = np.asarray(gathered, dtype=np.uint8).reshape(world, lay["size"])
+    out = []
+    for r in range(world):
+        lo, hi = proposer_range(n, world, r)
+        pos = lay["plain"][0]
+        for j in range(lo, hi):
+            out.append(g[r, pos:pos + int(lens[j])].tobytes())
+            pos += int(lens[j])
+    return out
+
+
 def assemble(gathered: np.ndarray, n: int, world: int):
     """Gathered slabs -> (share status uint8[n, n], ct status uint8[n], combine status int32[n]) in
     proposer order."""
     pm = max_columns(n, world)
     lay = slab_layout(n, pm)
-    g = np.asarray(gathered, dtype=np.uint8).reshape(world, lay["size"])
+    g = np.asarray(gathered, dtype=np.uint8).reshape(world, -1)[:, :lay["size"]]
     sv, cv, st = [], [], []
     for r in range(world):
         lo, hi = proposer_range(n, world, r)

@@ -39,3 +39,19 @@ def test_sharded_legs_world1(hbx_ctx):
         dist.destroy_process_group()
     assert c4["instances_per_gpu"] == 256 and c4["value"] > 0
     assert c5["instances_per_gpu"] == 128 and c5["value"] > 0
+
+
+@pytest.mark.gpu
+def test_strong_epoch_slab_world1():
+    """Stack A's strong-mode slab path (statuses + the plaintexts written straight into the
+    gathered slab, then assembled and compared with every contribution) at a world of one rank:
+    bench.py --strong-at-1 runs exactly the code --gpus G runs per rank."""
+    import json
+    import subprocess
+
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--strong-at-1", "--steps", "1", "--warmup", "0",
+                          "--configs=", "--no-cpu-baseline", "--in-flight", "1", "--n", "64"],
+                         capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["config"]["parallelism"] == "proposer-column x1" and line["value"] > 0

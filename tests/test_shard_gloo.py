@@ -40,6 +40,54 @@ def slab_for_slice(d, n, world, rank, share_status=None, ct_status=None, comb_st
     return slab
 
 
+def plain_slab(n, world, rank, lens, pb, seed=3):
+    """A slab with only the plaintext region filled: proposer j's plaintext = bytes of a seeded
+    stream of length lens[j] (what the rank's decryption writes there)."""
+    from hbbft_amd import shard
+
+    lay = shard.slab_layout(n, shard.max_columns(n, world), pb)
+    slab = np.zeros(lay["size"], dtype=np.uint8)
+    lo, hi = shard.proposer_range(n, world, rank)
+    pos = lay["plain"][0]
+    for j in range(lo, hi):
+        slab[pos:pos + lens[j]] = np.random.default_rng(seed + j).integers(0, 256, size=lens[j], dtype=np.uint8)
+        pos += lens[j]
+    return slab
+
+
+def _plain_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hbbft_amd import shard
+
+    n = 10
+    lens = [5 + 7 * j for j in range(n)]
+    pb = max(sum(lens[lo:hi]) for lo, hi in (shard.proposer_range(n, world, r) for r in range(world)))
+    g = shard.all_gather_slabs(torch.from_numpy(plain_slab(n, world, rank, lens, pb)), world)
+    got = shard.assemble_plaintexts(g.numpy(), n, world, lens, pb)
+    want = [np.random.default_rng(3 + j).integers(0, 256, size=lens[j], dtype=np.uint8).tobytes() for j in range(n)]
+    ss, cs, st = shard.assemble(g.numpy(), n, world)  # the status fields still assemble with the plaintext region
+    q.put((rank, got == want and ss.shape == (n, n)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_gather_plaintexts(world):
+    """The combined outputs of stack A -- every proposer's plaintext -- travel in the same
+    all-gather as the statuses (north_star: "validity bitmaps and combined outputs")."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plain_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
