@@ -222,7 +222,7 @@ def make_epoch(ctx, n: int, lo: int, hi: int, vlen: int, corrupt_every: int):
     ii = np.nonzero(corrupt)
     sh[ii[0], ii[1]] = shares[pj, ii[1]]
     return dict(pk_shares=pk_shares, cts=cts[:pj], msgs=msgs[:pj], shares=sh, corrupt=corrupt, t=sks.threshold + 1,
-                own_sk=sk_shares[OWN_INDEX].tobytes())
+                own_sk=sk_shares[OWN_INDEX].tobytes(), master_pk=master_pk)
 
 
 def cpu_baseline_dec(ep, seconds: float):
@@ -1169,6 +1169,17 @@ def main():
     pj = hi - lo
     ctx = Context(local)
     ep = make_epoch(ctx, n, lo, hi, args.vlen, args.corrupt_every)
+    key_ms = None
+    if world > 1:
+        # the node's key material reaches every rank in one broadcast per era from rank 0 (each
+        # rank synthesised the epoch's inputs itself; the engine is set up from what it received)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        pk, _mpk, own_sk, t_b = shard.broadcast_key_material(ep["pk_shares"], ep["master_pk"], ep["own_sk"], ep["t"], n,
+                                                             world, dev)
+        key_ms = round((time.perf_counter() - t0) * 1e3, 3)
+        assert (pk == ep["pk_shares"]).all() and own_sk == ep["own_sk"] and t_b == ep["t"], "era key broadcast"
+        ep["pk_shares"], ep["own_sk"], ep["t"] = pk, own_sk, t_b
     # a dedicated stream for the epoch calls; the HIP events that time the epoch and the kernels are
     # recorded on the stream the kernels run on
     stream = torch.cuda.Stream(dev)
@@ -1261,6 +1272,8 @@ def main():
         "roofline": verify_roofline(pj * n, kern["verify_shares"], kname, traffic),
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
     }
+    if key_ms is not None:
+        res["era_key_broadcast_ms"] = key_ms
     if world == 1 and args.in_flight > 1:
         res["epochs_in_flight"] = in_flight(args, eb, dev, torch, Context, verifies)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

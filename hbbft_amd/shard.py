@@ -80,6 +80,32 @@ def assemble_plaintexts(gathered: np.ndarray, n: int, world: int, lens, plain_by
     return out
 
 
+def broadcast_key_material(pk_comp, master_pk48: bytes, own_sk32: bytes, t: int, n: int, world: int, device,
+                           src: int = 0):
+    """Once per era (a key change is a new era, dynamic_honey_badger.rs): the node's key material
+    -- the N compressed public key shares (NetworkInfo, messaging.rs:251-254), the master public
+    key, this node's secret key share and the threshold -- from rank ``src`` to every rank in ONE
+    broadcast (RCCL on GPUs, gloo in the CPU tests), instead of each rank deriving it.  Other ranks
+    pass anything for the values (only ``n`` must agree).  Returns (pk_comp uint8[n, 48],
+    master_pk48, own_sk32, t)."""
+    import torch
+    import torch.distributed as dist
+
+    size = 4 + 48 + 32 + 48 * n
+    buf = np.zeros(size, dtype=np.uint8)
+    if world == 1 or dist.get_rank() == src:
+        buf[:4] = np.frombuffer(np.uint32(t).tobytes(), dtype=np.uint8)
+        buf[4:52] = np.frombuffer(bytes(master_pk48), dtype=np.uint8)
+        buf[52:84] = np.frombuffer(bytes(own_sk32), dtype=np.uint8)
+        buf[84:] = np.asarray(pk_comp, dtype=np.uint8).reshape(-1)
+    if world > 1:
+        tb = torch.from_numpy(buf).to(device)
+        dist.broadcast(tb, src)
+        buf = tb.cpu().numpy()
+    return (buf[84:].reshape(n, 48).copy(), buf[4:52].tobytes(), buf[52:84].tobytes(),
+            int(buf[:4].copy().view(np.uint32)[0]))
+
+
 def assemble(gathered: np.ndarray, n: int, world: int):
     """Gathered slabs -> (share status uint8[n, n], ct status uint8[n], combine status int32[n]) in
     proposer order."""

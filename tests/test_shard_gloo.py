@@ -88,6 +88,40 @@ def test_ranks_gather_plaintexts(world):
     assert res == {r: True for r in range(world)}
 
 
+def _keys_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hbbft_amd import shard
+
+    d = dict(np.load(FIX, allow_pickle=False))
+    n = int(d["n"])
+    mine = rank == 0
+    pk, mpk, sk, t = shard.broadcast_key_material(d["pk_comp"] if mine else np.zeros((n, 48), np.uint8),
+                                                  d["master_pk"].tobytes() if mine else bytes(48),
+                                                  d["own_sk"].tobytes() if mine else bytes(32),
+                                                  int(d["t"]) if mine else 0, n, world, torch.device("cpu"))
+    ok = (pk == d["pk_comp"]).all() and mpk == d["master_pk"].tobytes() and sk == d["own_sk"].tobytes() and t == int(d["t"])
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_key_material_broadcast(world):
+    """One broadcast per era gives every rank the node's key material (pk shares, master key,
+    own secret share, threshold) of rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_keys_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
