@@ -119,7 +119,7 @@ const char* hbx_version(void);
 #define HBX_K_RS_CODE 7         /* Reed-Solomon encode / reconstruct passes */
 #define HBX_K_MERKLE_LEAVES 8   /* SHA-256 leaf hashes */
 #define HBX_K_HASH_NONCES 9     /* coin nonce hash_g2 */
-#define HBX_K_DECODE_SIGS 10    /* coin signature-share decode (G2 decompression + subgroup check) */
+#define HBX_K_DECODE_SIGS 10    /* coin signature-share decode (G2 decompression; the checks test G2 membership) */
 #define HBX_K_COUNT 11
 int hbx_set_timing(hbx_ctx* ctx, int on);
 int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launches);
