@@ -90,6 +90,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per config")
     ap.add_argument("--verify-lanes", type=int, default=0, choices=(0, 1, 2, 3, 6, 7),
                     help="lanes per decryption-share check (0: auto by occupancy)")
+    ap.add_argument("--combine-lanes", type=int, default=0, choices=(0, 1, 4),
+                    help="lanes per Lagrange term in the combine (0: auto by occupancy)")
     ap.add_argument("--in-flight", type=int, default=2,
                     help="also time this many consecutive epochs in flight at once (one context and stream "
                          "each, as HoneyBadger's max_future_epochs allows); reported beside the headline")
@@ -325,9 +327,10 @@ def cpu_baseline_dec(ep, seconds: float):
 class EpochBench:
     """One node-epoch (or a proposer slice of one) on device-resident inputs, timed per step."""
 
-    def __init__(self, ctx, ep, dev, stream, torch, verify_lanes, own: bool):
+    def __init__(self, ctx, ep, dev, stream, torch, verify_lanes, own: bool, combine_lanes: int = 0):
         self.ctx, self.ep, self.dev, self.stream, self.torch = ctx, ep, dev, stream, torch
         ctx.set_verify_lanes(verify_lanes)
+        ctx.set_combine_lanes(combine_lanes)
         assert (ctx.set_pk_shares([row.tobytes() for row in ep["pk_shares"]]) == 0).all()
         if own:
             ctx.set_own_share(OWN_INDEX, ep["own_sk"])
@@ -1185,7 +1188,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
-    eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share)
+    eb = EpochBench(ctx, ep, dev, stream, torch, args.verify_lanes, not args.no_own_share, args.combine_lanes)
     # result slab gathered across ranks: [share status pj*n | ct status pj | combine status pj*4],
     # laid out for the largest column block so every rank's slab has the same size
     # ... and, at --gpus > 1, the plaintexts (the combined outputs): the rank's decryption blob IS
