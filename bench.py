@@ -591,7 +591,7 @@ def config_c4(args, dev, torch, Context):
         d_par = torch.zeros(inst, dtype=torch.uint8, device=dev)
 
         def round_():
-            ctx.prepare_nonces(nonces)
+            ctx.prepare_nonces(nonces, hashes=False)
             ctx.verify_sig_shares_d(d_bad, None, d_vst)
             ctx.combine_signatures_d(master_pk, t, None, d_sig, d_st, d_ok, d_par)
 
@@ -1075,7 +1075,7 @@ def sharded_c4(args, dev, torch, Context, world, rank):
         gathered = [None]
 
         def step():
-            ctx.prepare_nonces(nonces)
+            ctx.prepare_nonces(nonces, hashes=False)
             ctx.verify_sig_shares_d(d_bad, None, v["share_status"])
             ctx.combine_signatures_d(master_pk, t, None, v["sig"], v["comb_status"], v["master_ok"], v["parity"])
             gathered[0] = shard.all_gather_slabs(slab, world)

@@ -67,7 +67,7 @@ class GpuCoinEngine:
         self.count = 0
 
     def prepare(self, nonces):
-        self.ctx.prepare_nonces([bytes(x) for x in nonces])
+        self.ctx.prepare_nonces([bytes(x) for x in nonces], hashes=False)
         self.count = len(nonces)
 
     def sign(self) -> np.ndarray:

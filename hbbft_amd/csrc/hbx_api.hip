@@ -57,8 +57,7 @@ struct dbuf {
 struct hbx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t aux_stream = nullptr;      // side work of hbx_prepare_nonces (the true H)
-  hipEvent_t aux_ev[2] = {nullptr, nullptr};
+  bool coin_h_ready = false;  // coin_H (the true hash_g2 of the prepared nonces) computed
   hipEvent_t coin_ready_ev = nullptr;  // end of hbx_prepare_nonces' work: later coin calls on any stream wait on it
   std::string err = "ok";
   int digest = DIGEST_SHA256;         // hbx_set_digest: threshold_crypto's DIGEST
@@ -490,10 +489,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipEventDestroy(c->ev_last);
-  if (c->aux_ev[0]) (void)hipEventDestroy(c->aux_ev[0]);
-  if (c->aux_ev[1]) (void)hipEventDestroy(c->aux_ev[1]);
   if (c->coin_ready_ev) (void)hipEventDestroy(c->coin_ready_ev);
-  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return HBX_OK;
@@ -1046,6 +1042,16 @@ int hbx_broadcast_decode_leaves_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* 
 }
 
 // ---- Common Coin ----------------------------------------------------------------------------
+// The true H = hash_g2(nonce) of the prepared nonces from H' = [m] H (k_h2_from_heff), once, on s.
+static int coin_true_h(hbx_ctx* c, hipStream_t s) {
+  if (c->coin_h_ready) return HBX_OK;
+  hipLaunchKernelGGL(k_h2_from_heff, dim3((c->coin_I + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), c->coin_I,
+                     c->coin_H.as<g2a>());
+  HIPCHK(c, hipGetLastError());
+  c->coin_h_ready = true;
+  return HBX_OK;
+}
+
 int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* nonce_off, uint32_t count,
                        uint8_t* h96) {
   if (!c || !nonce_off || count == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_prepare_nonces: bad args");
@@ -1073,23 +1079,14 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
                        c->coin_off.as<uint64_t>(), count, c->coin_Hp.as<g2a>(), c->digest, 0);
   }
   HIPCHK(c, hipGetLastError());
-  // the true H (for hbx_sign and h96) on the auxiliary stream, beside the line preparation
-  if (!c->aux_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-  if (!c->aux_ev[0]) {
-    HIPCHK(c, hipEventCreateWithFlags(&c->aux_ev[0], hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->aux_ev[1], hipEventDisableTiming));
-  }
-  HIPCHK(c, hipEventRecord(c->aux_ev[0], s));
-  HIPCHK(c, hipStreamWaitEvent(c->aux_stream, c->aux_ev[0], 0));
-  hipLaunchKernelGGL(k_h2_from_heff, dim3((count + 63) / 64), dim3(64), 0, c->aux_stream, c->coin_Hp.as<g2a>(), count,
-                     c->coin_H.as<g2a>());
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->aux_ev[1], c->aux_stream));
   // the Miller lines of H' are prepared on demand by the one-lane share checks (the two-lane
-  // kernel, the default for a coin round, generates both pairs' lines itself)
+  // kernel, the default for a coin round, generates both pairs' lines itself); the true H only for
+  // hbx_sign and h96 (coin_true_h): the share checks and the combine work on H' = [m] H
   c->coin_lines_ready = false;
-  HIPCHK(c, hipStreamWaitEvent(s, c->aux_ev[1], 0));  // the true H is in
+  c->coin_h_ready = false;
+  c->coin_I = count;
   if (h96) {
+    if (int rc = coin_true_h(c, s)) return rc;
     hipLaunchKernelGGL(k_compress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->coin_H.as<g2a>(), count, 1u,
                        c->coin_out96.as<uint8_t>());
     HIPCHK(c, hipGetLastError());
@@ -1113,6 +1110,7 @@ int hbx_sign(hbx_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* sig96) {
   if (!c->coin_sk.ensure((size_t)n * 32) || !c->coin_sig96.ensure(m * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_sign: out of device memory");
   HIPCHK(c, hipMemcpyAsync(c->coin_sk.p, sk32, (size_t)n * 32, hipMemcpyHostToDevice, s));
+  if (int rc = coin_true_h(c, s)) return rc;
   hipLaunchKernelGGL(k_sign, dim3((n + 63) / 64, c->coin_I), dim3(64), 0, s, c->coin_sk.as<uint8_t>(), n,
                      c->coin_H.as<g2a>(), c->coin_sig96.as<uint8_t>());
   HIPCHK(c, hipGetLastError());

@@ -406,15 +406,17 @@ class Context:
             None if d_valid is None else d_valid.data_ptr(), self._stream(stream)))
 
     # -- common coin ------------------------------------------------------------------------------
-    def prepare_nonces(self, nonces: Sequence[bytes]) -> np.ndarray:
-        """hash_g2 of every nonce (+ prepared lines); returns uint8[count, 96] compressed points."""
+    def prepare_nonces(self, nonces: Sequence[bytes], hashes: bool = True) -> Optional[np.ndarray]:
+        """hash_g2 of every nonce; returns uint8[count, 96] compressed points, or None with
+        ``hashes=False`` -- then the call returns after its uploads, the share checks and the
+        combine do not wait for the true H (only hbx_sign does), and the hashing runs on."""
         count = len(nonces)
         off = np.zeros(count + 1, dtype=np.uint64)
         off[1:] = np.cumsum([len(x) for x in nonces])
         blob = np.frombuffer(b"".join(nonces) or b"\0", dtype=np.uint8).copy()
-        h = np.zeros((count, 96), dtype=np.uint8)
+        h = np.zeros((count, 96), dtype=np.uint8) if hashes else None
         self._check(self.lib.hbx_prepare_nonces(self.h, _u8(blob), off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-                                                count, _u8(h)))
+                                                count, _u8(h) if hashes else None))
         self._coin_count = count
         return h
 

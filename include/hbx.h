@@ -281,7 +281,10 @@ int hbx_decrypt_shares(hbx_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint
  * Common Coin, batched over `count` coin instances (concurrent
  * Agreement instances; the nonce of each is Nonce::new, src/agreement/mod.rs:155-165).
  * hbx_prepare_nonces -- hash_g2(nonce_i) once per instance (threshold_crypto, hoisted out of
- *   every share verification) + its prepared Miller lines; h96 (optional) = the compressed points.
+ *   every share verification); h96 (optional) = the compressed points.  The call returns once the
+ *   nonces are uploaded (with h96, once the hashes are in h96); later coin calls on any stream are
+ *   ordered after the hashing, and only hbx_sign waits for the true H (the checks and the combine
+ *   work on [m] H).
  * hbx_sign -- SecretKeyShare::sign (src/common_coin.rs:142): sig96[inst][i] = sk_i * hash_g2(nonce).
  * hbx_verify_sig_shares -- PublicKeyShare::verify (src/common_coin.rs:151) for a [count][n] matrix
  *   of compressed signature shares (present_bits NULL = all present); uses hbx_set_pk_shares keys.
