@@ -763,12 +763,20 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
   // profiles/r03a_bench.json), so it is only used when asked for.
   {
     timed t_(c, HBX_K_VERIFY_SHARES, s);
+    // below a full chip: the most lanes per check that still fit one wave per SIMD -- six, three,
+    // then two (an N=256 epoch over 2 GPUs: 1,024 two-lane waves, 11.0 ms against 17.4 for the
+    // three-lane check in two rounds of waves, profiles/r04w_lanes.txt)
     const size_t waves1 = (size_t)((n + 63) / 64) * p;
+    const size_t waves2 = (size_t)((n + 31) / 32) * p;
+    const size_t waves3 = (size_t)((n + G3_PER_WAVE - 1) / G3_PER_WAVE) * p;
     const size_t waves6 = (size_t)((n + G6_PER_WAVE - 1) / G6_PER_WAVE) * p;
-    const int lanes = c->verify_lanes                           ? c->verify_lanes
-                      : waves1 >= (size_t)VERIFY_FILL_WAVES   ? 1
-                      : waves6 <= (size_t)VERIFY_FILL_WAVES   ? 6
-                                                              : 3;
+    const size_t fill = (size_t)VERIFY_FILL_WAVES;
+    const int lanes = c->verify_lanes   ? c->verify_lanes
+                      : waves1 >= fill ? 1
+                      : waves6 <= fill ? 6
+                      : waves3 <= fill ? 3
+                      : waves2 <= fill ? 2
+                                       : 3;
     c->lanes_used = lanes;
     if (lanes == 2) {
       // global slots of the final exponentiation: 2 x 78 dwords per lane of the launch
