@@ -536,6 +536,55 @@ HBX_HD fq fqd_to_fq(const fqd& a) {
   return fq_csub(r, FQ_2P);
 }
 HBX_HD fq2d fq2d_from_fq2(const fq2& a) { return fq2d{fqd_from_fq(a.c0), fqd_from_fq(a.c1)}; }
+
+// a^e (e a 384-bit constant, 12 LE words) in the digit tower: field.hpp fq_pow_const's 4-bit
+// fixed windows, with the squarings and products as fqd_sqr / fqd_mul (no re-cutting of 12 limbs
+// into digits around every product).  In and out in field.hpp's 12-limb form.  The hash chains'
+// square roots (hash.hpp hash_g2_group) run on it.
+HBX_HDNI fq fq_pow_const_d(const fq& a_, const uint32_t* e) {
+  const fqd a = fqd_from_fq(a_);
+  fqd tab[16];
+  tab[0] = fqd_const(FQD_ONE);
+  tab[1] = a;
+  for (int i = 2; i < 16; i++) tab[i] = fqd_mul(tab[i - 1], a);
+  fqd r = tab[0];
+  bool started = false;
+  for (int w = 95; w >= 0; w--) {
+    const uint32_t nib = (e[w >> 3] >> ((w & 7) * 4)) & 0xF;
+    if (started) {
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) r = fqd_sqr(r);
+    }
+    if (nib) {
+      fqd t = tab[1];
+      for (int k = 2; k < 16; k++)
+        if ((uint32_t)k == nib) t = tab[k];
+      r = started ? fqd_mul(r, t) : t;
+      started = true;
+    }
+  }
+  return fqd_to_fq(r);
+}
+// field.hpp fq_sqrt / fq2_norm_sqrt / fq2_sqrt_from_norm with fq_pow_const_d
+HBX_HD bool fq_sqrt_d(const fq& a, fq& out) {
+  const fq s = fq_pow_const_d(a, FQ_SQRT_EXP);
+  out = s;
+  return fq_eq(fq_sqr(s), a);
+}
+HBX_HD bool fq2_norm_sqrt_d(const fq2& a, fq& s) {
+  const fq n = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+  return fq_sqrt_d(n, s);
+}
+HBX_HDNI fq2 fq2_sqrt_from_norm_d(const fq2& a, const fq& s) {
+  const fq half = fq_from_const(FQ_HALF_MONT);
+  const fq alpha = fq_mul(fq_add(a.c0, s), half);
+  const fq e = fq_pow_const_d(alpha, FQ_P_MINUS_3_DIV_4);
+  const fq t = fq_mul(alpha, e);
+  const fq c = fq_mul(t, e);
+  const fq h = fq_mul(fq_mul(a.c1, e), half);
+  if (fq_eq(c, fq_one())) return fq2{t, h};
+  return fq2{fq_neg(h), t};
+}
 HBX_HD fq2 fq2d_to_fq2(const fq2d& a) { return fq2{fqd_to_fq(a.c0), fqd_to_fq(a.c1)}; }
 HBX_HD fq6d fq6d_from_fq6(const fq6& a) { return fq6d{fq2d_from_fq2(a.c0), fq2d_from_fq2(a.c1), fq2d_from_fq2(a.c2)}; }
 HBX_HD fq6 fq6d_to_fq6(const fq6d& a) { return fq6{fq2d_to_fq2(a.c0), fq2d_to_fq2(a.c1), fq2d_to_fq2(a.c2)}; }

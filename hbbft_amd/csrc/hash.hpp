@@ -10,6 +10,7 @@
 //    lift, multiply by the full cofactor h2, retry).
 #pragma once
 #include "curve.hpp"
+#include "fieldd.hpp"
 #include "dpp.hpp"
 
 namespace hbx {
@@ -556,7 +557,7 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out, bool fu
     fq2 y0 = fq2_zero();
     bool sq;
     if (c1zero) sq = fq2_sqrt(rhs, y0);  // measure-zero branch, exact general square root
-    else sq = fq2_norm_sqrt(rhs, s);
+    else sq = fq2_norm_sqrt_d(rhs, s);
     HBX_PHASE(2);
     const uint64_t pass = __ballot(sq) & gmask;
     if (pass == 0) {
@@ -566,7 +567,7 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out, bool fu
     const int win = __builtin_ctzll(pass) - gbase;
     fq2 y = fq2_zero();
     if (gl == win) {
-      y = c1zero ? y0 : fq2_sqrt_from_norm(rhs, s);
+      y = c1zero ? y0 : fq2_sqrt_from_norm_d(rhs, s);
       // pairing: y if (y < -y) ^ greatest else -y  ==  pick the larger root iff greatest
       if (fq2_lex_largest(y) != greatest) y = fq2_neg(y);
     }

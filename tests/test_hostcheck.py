@@ -421,3 +421,12 @@ def test_miller_gen_matches_mixed(hc):
         q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
         assert hc.hc_miller_gen_cmp(q, 0) == 1
         assert hc.hc_miller_gen_cmp(q, 1) == 1  # (qx, qy, bx, by) parked in the lane's slot
+
+
+def test_digit_tower_square_roots(hc):
+    """hash_g2_group's square roots with the digit-tower exponentiation equal field.hpp's."""
+    hc.hc_sqrt_d_cmp.argtypes = [ctypes.c_char_p]
+    rnd = random.Random(21)
+    for _ in range(12):
+        x = rnd.randrange(1, bls.P)
+        assert hc.hc_sqrt_d_cmp(x.to_bytes(48, "big")) == 1

@@ -348,3 +348,22 @@ int hc_miller_gen_cmp(const uint8_t* q96, int parked) {
   return g2j_eq(t1, t2) ? 1 : 0;
 }
 }
+extern "C" {
+// the digit-tower square roots of the hash chains against field.hpp's: 1 if all agree
+int hc_sqrt_d_cmp(const uint8_t* x48) {
+  fq a = fq_to_mont(fq_from_be(x48));
+  fq s1, s2;
+  const bool r1 = fq_sqrt(a, s1), r2 = fq_sqrt_d(a, s2);
+  if (r1 != r2 || (r1 && !fq_eq(fq_canon(s1), fq_canon(s2)))) return 0;
+  const fq2 b{a, fq_add(a, fq_one())};
+  fq n1, n2;
+  const bool q1 = fq2_norm_sqrt(b, n1), q2 = fq2_norm_sqrt_d(b, n2);
+  if (q1 != q2) return 0;
+  if (q1) {
+    if (!fq_eq(fq_canon(n1), fq_canon(n2))) return 0;
+    const fq2 y1 = fq2_sqrt_from_norm(b, n1), y2 = fq2_sqrt_from_norm_d(b, n2);
+    if (!fq_eq(fq_canon(y1.c0), fq_canon(y2.c0)) || !fq_eq(fq_canon(y1.c1), fq_canon(y2.c1))) return 0;
+  }
+  return 1;
+}
+}
