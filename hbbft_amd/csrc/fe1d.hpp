@@ -300,8 +300,19 @@ HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
 template <int S, int SG, class P, class PG>
 HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3, bool& degenerate) {
   static_assert(BLS_X == 0xd201000000010000ull, "square-and-multiply runs are specific to |x|");
+  int q0 = 0;
+  if (t3) {
+    // the first run (one squaring) and its product outside the loop, so that the loop body holds
+    // no store of r (with it inside, F1 spilled 446 VGPRs against F2's 132)
+    r = fq12d_cyclotomic_sqr_seq(r);
+    HBX_SEQ();
+    r = fq12d_mul_slot<S>(r, a);
+    HBX_SEQ();
+    s1_put_fq12d<SG>(t3, r);
+    q0 = 1;
+  }
 #pragma unroll 1
-  for (int q = 0; q < 6; q++) {
+  for (int q = q0; q < 6; q++) {
     const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
     if (q >= 3) {
       fq12c c{r.c0.c1, r.c0.c2, r.c1.c0, r.c1.c2};
@@ -316,7 +327,6 @@ HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3, bool& degenerate) {
     if (q < 5) {
       HBX_SEQ();
       r = fq12d_mul_slot<S>(r, a);
-      if (q == 0 && t3) s1_put_fq12d<SG>(t3, r);
     }
   }
   return r;
@@ -419,9 +429,39 @@ HBX_HD bool fq12d_is_one_seq(const fq12d& a) {
 // (Miller output, later b), T (t^3, later d), G (t, a, u) ------------------------------------------
 constexpr int FE1_STEPS = 7;
 // F0: t = frob2(t0) t0, t0 = conj(f) / f  -> G
+template <int SG, class PG>
+HBX_HD fq6d s1_get_half(PG p, int h) {
+  return fq6d{s1_get_fq2d<SG>(p, 3 * h), s1_get_fq2d<SG>(p, 3 * h + 1), s1_get_fq2d<SG>(p, 3 * h + 2)};
+}
+// fe1_easy_first restated over the slots, so that f never sits in registers beside the products
+// (it held f, g and the accumulators at once: 718 VGPRs spilled): N(f) from f's halves one at a
+// time, N^-1 into slot a, g = conj(f)^2 parked in slot G (overwritten at the end), each half of
+// g times N^-1 streamed from a.
 template <int S, int SG, class P, class PG>
 HBX_HD void fe1_step0(P a, PG gf, PG gg) {
-  fq12d r = fe1_easy_first<S>(s1_get_fq12d<SG>(gf), a);  // t0
+  {
+    fq6d n;
+    {
+      const fq6d f0 = s1_get_half<SG>(gf, 0);
+      n = fq6d_mul(f0, f0);
+    }
+    HBX_SEQ();
+    {
+      const fq6d f1 = s1_get_half<SG>(gf, 1);
+      n = fq6d_reduce(fq6d_sub(n, fq6d_mul_v(fq6d_mul(f1, f1))));
+    }
+    HBX_SEQ();
+    fq6d_inv_to_slot<S>(n, a);  // words [0, 78): N^-1
+  }
+  HBX_SEQ();
+  s1_put_fq12d<SG>(gg, fq12d_sqr(fq12d_conj(s1_get_fq12d<SG>(gf))));  // g
+  HBX_SEQ();
+  fq6d A = fq6d_zero_();
+  fq6d_mul_acc1(A, s1_get_half<SG>(gg, 0), [&](int q) { return s1_get_fq2d<S>(a, q); });
+  HBX_SEQ();
+  fq6d B = fq6d_zero_();
+  fq6d_mul_acc1(B, s1_get_half<SG>(gg, 1), [&](int q) { return s1_get_fq2d<S>(a, q); });
+  fq12d r{fq6d_reduce(A), fq6d_reduce(B)};  // t0 = conj(f) / f
   HBX_SEQ();
   s1_put_fq12d<S>(a, r);
   HBX_SEQ();
