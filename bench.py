@@ -145,6 +145,14 @@ def quota_cores():
         return None
 
 
+def hbx_build_info():
+    """Provenance of the loaded libhbx.so (hbbft_amd/hbx.py build_info: compiled-in source hash vs
+    the tree's)."""
+    from hbbft_amd import hbx
+
+    return hbx.build_info()
+
+
 def traffic_record():
     """Newest PMC record for the share check (profiles/*_pmc_hbm.json), or None."""
     import glob
@@ -1274,6 +1282,7 @@ def main():
         "verify_lanes": lanes,
         "roofline": verify_roofline(pj * n, kern["verify_shares"], kname, traffic),
         "check": "validity bitmap == not-corrupted; plaintexts == contributions",
+        "build": hbx_build_info(),
     }
     if key_ms is not None:
         res["era_key_broadcast_ms"] = key_ms

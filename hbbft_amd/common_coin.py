@@ -235,7 +235,7 @@ class CoinReplay:
             b.terminated = True
             res.outputs.append((inst, par))
 
-        def handle_share(inst, sender, m):
+        def handle_share(inst, sender, m, who):
             b = insts[inst]
             st = status[m]
             if st != SHARE_VALID:
@@ -243,7 +243,7 @@ class CoinReplay:
                     res.faults.append((sender, UNVERIFIED_SIGNATURE_SHARE_SENDER))
                 return
             b.received[sender] = m
-            try_output(inst, sender)
+            try_output(inst, who)
 
         for k, ev in enumerate(events):
             if ev[0] == "input":
@@ -256,8 +256,12 @@ class CoinReplay:
                     try_output(inst, None)
                     continue
                 m = msg_of_event[k]
-                res.sent.append((inst, msgs[m][2]))
-                handle_share(inst, self.me, m)
+                # get_coin (common_coin.rs:142-146): an error from our own share's handle_share
+                # drops the step with the outgoing message (the `?`); the error is our input's
+                n_err = len(res.errors)
+                handle_share(inst, self.me, m, None)
+                if len(res.errors) == n_err:
+                    res.sent.append((inst, msgs[m][2]))
             else:
                 _, sender, inst, _ = ev
                 b = insts[inst]
@@ -268,7 +272,7 @@ class CoinReplay:
                 if not 0 <= sender < self.n:
                     res.errors.append((sender, UNKNOWN_SENDER))
                     continue
-                handle_share(inst, sender, msg_of_event[k])
+                handle_share(inst, sender, msg_of_event[k], sender)
         return res, pending
 
     def _combine(self, pending, msgs, layer_of, known, count):

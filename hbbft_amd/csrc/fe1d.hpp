@@ -233,8 +233,10 @@ HBX_HD fq12d fq12d_cyclotomic_sqr_seq(const fq12d& f) {
 // (2 g1 g5 = (g1 + g5)^2 - g1^2 - g5^2, 2 g2 g3 likewise).  Decompression recovers
 //   g4 = c1.c1 = (xi g5^2 + 3 g1^2 - 2 g2) / (4 g3),   g0 = c0.c0 = xi (2 g4^2 + g3 g5 - 3 g1 g2) + 1,
 // one Fq2 inversion per run (checked against the oracle's squarings, tools/hostcheck).  g3 = 0
-// makes the division impossible (an event of probability ~2^-760 per run, not reachable by
-// choosing shares); such a lane is flagged and re-checked by the single-kernel path.
+// makes the division impossible; such a lane is flagged and re-checked by the single-kernel path.
+// For a run that starts at the identity (t = 1 after the easy part) g3 = 0 always: a proposer can
+// cause that on purpose (fe1_step0 explains how), so step 0 decides t = 1 itself.  Otherwise g3 = 0
+// needs an element with a zero Fq2 coefficient at a run's end (~2^-760 for values not chosen so).
 struct fq12c {
   fq2d g1, g2, g3, g5;
 };
@@ -438,7 +440,7 @@ HBX_HD fq6d s1_get_half(PG p, int h) {
 // time, N^-1 into slot a, g = conj(f)^2 parked in slot G (overwritten at the end), each half of
 // g times N^-1 streamed from a.
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step0(P a, PG gf, PG gg) {
+HBX_HD bool fe1_step0(P a, PG gf, PG gg) {
   {
     fq6d n;
     {
@@ -467,6 +469,12 @@ HBX_HD void fe1_step0(P a, PG gf, PG gg) {
   HBX_SEQ();
   r = fq12d_mul_slot<S>(fq12d_frobenius2(r), a);
   s1_put_fq12d<SG>(gg, r);
+  HBX_SEQ();
+  // t = 1: the hard part of 1 is 1, so the check holds and no compressed squaring runs (they would
+  // start at g3 = 0 and send the lane to the fallback).  Reachable on purpose: a ciphertext with
+  // r = 3(x^2 - 1) makes W = H' and every honest share S_i = [m] pk_i, so f = f_H'(P) f_H'(-P) lies
+  // in Fq6 and t = 1 (tests/test_gpu_threshold.py::test_degenerate_ciphertext_r_m).
+  return fq12d_is_one_seq(r);
 }
 // F1, F2: x -> conj(x^|x| x) (x = t: t^3 -> T on the way; then x = a)
 template <int S, int SG, class P, class PG>

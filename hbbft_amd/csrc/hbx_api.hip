@@ -89,6 +89,9 @@ struct hbx_ctx {
   dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
   dbuf fe1slot;  // one-lane checks: the final exponentiation's global slots F, T, G (fe1d.hpp)
   uint32_t force_fallback = 0;  // hbx_debug_force_fallback (tests only)
+  dbuf fb_lanes;                // u32: lanes the last one-lane launch's fallback check decided
+  dbuf hs[6];                   // staging of the host-pointer broadcast calls
+  bool fb_lanes_valid = false;  // fb_lanes was reset by a one-lane launch
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -441,6 +444,10 @@ static int merkle_roots(hbx_ctx* c, const uint8_t* d_shards, uint32_t inst, uint
 extern "C" {
 
 const char* hbx_version(void) { return "hbx 0.1.0 gfx950"; }
+#ifndef HBX_SOURCE_HASH
+#define HBX_SOURCE_HASH "unknown"
+#endif
+const char* hbx_build_id(void) { return HBX_SOURCE_HASH; }
 
 const char* hbx_last_error(const hbx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
@@ -485,7 +492,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
                   &c->vs_pk, &c->vs_lines_d, &c->coin_lines_d, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
-                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->fe1slot, &c->coin_use, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
+                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->fe1slot, &c->fb_lanes, &c->hs[0], &c->hs[1], &c->hs[2], &c->hs[3], &c->hs[4], &c->hs[5], &c->coin_use, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipEventDestroy(c->ev_last);
@@ -521,6 +528,16 @@ int hbx_debug_force_fallback(hbx_ctx* c, uint32_t every) {
   if (!c) return HBX_E_INVALID_ARG;
   c->force_fallback = every;
   return HBX_OK;
+}
+
+int64_t hbx_get_fallback_lanes(hbx_ctx* c) {
+  if (!c) return HBX_E_INVALID_ARG;
+  if (!c->fb_lanes_valid) return 0;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, quiesce(c));
+  uint32_t v = 0;
+  HIPCHK(c, hipMemcpy(&v, c->fb_lanes.p, 4, hipMemcpyDeviceToHost));
+  return v;
 }
 
 int hbx_set_combine_lanes(hbx_ctx* c, int lanes) {
@@ -806,7 +823,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          c->S_status.as<int32_t>(), d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(),
                          c->lines_d.as<line_block_d>(), c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(),
                          own ? c->own_me : UINT32_MAX,
-                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, 0u);
+                         (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, 0u, nullptr);
     else {
       // one lane per check: the Miller loops, then the final exponentiation as seven step kernels
       // over per-lane slots (fe1d.hpp: no Fq12 ever crosses a call frame)
@@ -816,6 +833,9 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
       uint8_t* ctv = (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr;
       const uint32_t me = own ? c->own_me : UINT32_MAX;
       uint32_t* gs = c->fe1slot.as<uint32_t>();
+      if (!c->fb_lanes.ensure(4)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
+      HIPCHK(c, hipMemsetAsync(c->fb_lanes.p, 0, 4, s));
+      c->fb_lanes_valid = true;
       hipLaunchKernelGGL(k_verify_shares_ml, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(),
                          d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(),
                          c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(), me, gs);
@@ -831,7 +851,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
       // lanes whose compressed squarings met g3 = 0 (never expected): the single-kernel check
       hipLaunchKernelGGL(k_verify_shares, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present,
                          c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), ctok, n, vd,
-                         me, ctv, 1u);
+                         me, ctv, 1u, c->fb_lanes.as<uint32_t>());
     }
   }
   HIPCHK(c, hipGetLastError());
@@ -1049,6 +1069,202 @@ int hbx_broadcast_decode_leaves_d(hbx_ctx* c, uint8_t* d_shards, const uint8_t* 
                           d_out_len, d_status, stream);
 }
 
+// ---- Broadcast, host-pointer forms (include/hbx.h): the _d calls above on context-owned staging
+// buffers (c->hs[]), on the context's own stream, blocking until the outputs are on the host -- the
+// shape a thin Rust FFI drives from Vec<u8> / &[u8] ------------
+static uint8_t* stage(hbx_ctx* c, int slot, size_t bytes) {
+  return c->hs[slot].ensure(bytes ? bytes : 1) ? c->hs[slot].as<uint8_t>() : nullptr;
+}
+#define HBX_STAGE(ptr, slot, bytes, what)                                                      \
+  uint8_t* ptr = stage(c, slot, bytes);                                                      \
+  if (!ptr) return fail(c, HBX_E_OUT_OF_MEMORY, "%s: out of device memory (staging)", what)
+#define HBX_H2D(dst, src, bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream))
+#define HBX_D2H(dst, src, bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream))
+
+int hbx_rs_encode(hbx_ctx* c, uint8_t* shards, uint32_t inst, uint32_t k, uint32_t m, uint32_t L) {
+  if (!c || !shards || inst == 0 || L == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_rs_encode: bad args");
+  if (m == 0) return HBX_OK;  // Coding::Trivial
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t row = (size_t)(k + m) * L;
+  HBX_STAGE(d, 0, row * inst, "hbx_rs_encode");
+  // the k data shards of every instance in, the m parity shards out (one strided copy each way)
+  HIPCHK(c, hipMemcpy2DAsync(d, row, shards, row, (size_t)k * L, inst, hipMemcpyHostToDevice, c->stream));
+  int rc = hbx_rs_encode_d(c, d, inst, k, m, L, c->stream);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy2DAsync(shards + (size_t)k * L, row, d + (size_t)k * L, row, (size_t)m * L, inst,
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_rs_reconstruct(hbx_ctx* c, uint8_t* shards, const uint8_t* present, uint32_t inst, uint32_t k, uint32_t m,
+                       uint32_t L, int32_t* status) {
+  if (!c || !shards || !present || !status || inst == 0 || L == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_rs_reconstruct: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t n = (size_t)k + m, all = n * L * inst;
+  HBX_STAGE(d, 0, all, "hbx_rs_reconstruct");
+  HBX_STAGE(dp, 1, n * inst, "hbx_rs_reconstruct");
+  HBX_STAGE(ds, 2, (size_t)inst * 4, "hbx_rs_reconstruct");
+  HBX_H2D(d, shards, all);
+  HBX_H2D(dp, present, n * inst);
+  int rc = hbx_rs_reconstruct_d(c, d, dp, inst, k, m, L, (int32_t*)ds, c->stream);
+  if (rc) return rc;
+  HBX_D2H(shards, d, all);
+  HBX_D2H(status, ds, (size_t)inst * 4);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_merkle_roots(hbx_ctx* c, const uint8_t* shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* roots) {
+  if (!c || !shards || !roots || inst == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_roots: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t all = (size_t)n * L * inst;
+  HBX_STAGE(d, 0, all, "hbx_merkle_roots");
+  HBX_STAGE(dr, 1, (size_t)inst * 32, "hbx_merkle_roots");
+  HBX_H2D(d, shards, all);
+  int rc = hbx_merkle_roots_d(c, d, inst, n, L, dr, c->stream);
+  if (rc) return rc;
+  HBX_D2H(roots, dr, (size_t)inst * 32);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_merkle_build(hbx_ctx* c, const uint8_t* shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* nodes,
+                     uint8_t* roots) {
+  if (!c || !shards || !nodes || inst == 0 || n == 0) return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_build: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t all = (size_t)n * L * inst, nb = (size_t)inst * merkle_node_count(n) * 32;
+  HBX_STAGE(d, 0, all, "hbx_merkle_build");
+  HBX_STAGE(dn, 1, nb, "hbx_merkle_build");
+  HBX_STAGE(dr, 2, (size_t)inst * 32, "hbx_merkle_build");
+  HBX_H2D(d, shards, all);
+  int rc = hbx_merkle_build_d(c, d, inst, n, L, dn, dr, c->stream);
+  if (rc) return rc;
+  HBX_D2H(nodes, dn, nb);
+  if (roots) HBX_D2H(roots, dr, (size_t)inst * 32);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_merkle_proofs(hbx_ctx* c, const uint8_t* nodes, uint32_t inst, uint32_t n, const uint32_t* req, uint32_t count,
+                      uint8_t* node_hash, uint8_t* sib_hash, uint32_t* sides, uint32_t* depth, uint8_t* root) {
+  if (!c || !nodes || !req || !node_hash || !sib_hash || !sides || !depth || !root || inst == 0 || count == 0 ||
+      n == 0 || n > (uint32_t)RS_MAX_N)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_proofs: bad args");
+  for (uint32_t q = 0; q < count; q++)
+    if (req[2 * q] >= inst || req[2 * q + 1] >= n)
+      return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_proofs: request %u names leaf %u of instance %u (inst %u, n %u)",
+                  q, req[2 * q + 1], req[2 * q], inst, n);
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t nb = (size_t)inst * merkle_node_count(n) * 32;
+  HBX_STAGE(dn, 0, nb, "hbx_merkle_proofs");
+  HBX_STAGE(dq, 1, (size_t)count * 8, "hbx_merkle_proofs");
+  HBX_STAGE(dh, 2, (size_t)count * 17 * 32, "hbx_merkle_proofs");
+  HBX_STAGE(dsib, 3, (size_t)count * 16 * 32, "hbx_merkle_proofs");
+  HBX_STAGE(dsd, 4, (size_t)count * 8, "hbx_merkle_proofs");
+  HBX_STAGE(dr, 5, (size_t)count * 32, "hbx_merkle_proofs");
+  HBX_H2D(dn, nodes, nb);
+  HBX_H2D(dq, req, (size_t)count * 8);
+  int rc = hbx_merkle_proofs_d(c, dn, n, (const uint32_t*)dq, count, dh, dsib, (uint32_t*)dsd,
+                               (uint32_t*)dsd + count, dr, c->stream);
+  if (rc) return rc;
+  HBX_D2H(node_hash, dh, (size_t)count * 17 * 32);
+  HBX_D2H(sib_hash, dsib, (size_t)count * 16 * 32);
+  HBX_D2H(sides, dsd, (size_t)count * 4);
+  HBX_D2H(depth, dsd + (size_t)count * 4, (size_t)count * 4);
+  HBX_D2H(root, dr, (size_t)count * 32);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_merkle_validate(hbx_ctx* c, const uint8_t* values, uint32_t vlen, const uint8_t* node_hash,
+                        const uint8_t* sib_hash, const uint32_t* sides, const uint32_t* depth, const uint8_t* root,
+                        const uint32_t* sender, uint32_t count, uint32_t nproofs, uint8_t* valid) {
+  if (!c || !values || !node_hash || !sib_hash || !sides || !depth || !root || !sender || !valid || nproofs == 0 ||
+      vlen == 0)
+    return fail(c, HBX_E_INVALID_ARG, "hbx_merkle_validate: bad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t P = nproofs;
+  HBX_STAGE(dv, 0, P * vlen, "hbx_merkle_validate");
+  HBX_STAGE(dh, 1, P * 17 * 32, "hbx_merkle_validate");
+  HBX_STAGE(dsib, 2, P * 16 * 32, "hbx_merkle_validate");
+  HBX_STAGE(du, 3, P * 12, "hbx_merkle_validate");  // sides | depth | sender
+  HBX_STAGE(dr, 4, P * 32, "hbx_merkle_validate");
+  HBX_STAGE(dok, 5, P, "hbx_merkle_validate");
+  HBX_H2D(dv, values, P * vlen);
+  HBX_H2D(dh, node_hash, P * 17 * 32);
+  HBX_H2D(dsib, sib_hash, P * 16 * 32);
+  HBX_H2D(du, sides, P * 4);
+  HBX_H2D(du + P * 4, depth, P * 4);
+  HBX_H2D(du + P * 8, sender, P * 4);
+  HBX_H2D(dr, root, P * 32);
+  const uint32_t* u = (const uint32_t*)du;
+  int rc = hbx_merkle_validate_d(c, dv, vlen, dh, dsib, u, u + P, dr, u + 2 * P, count, nproofs, dok, c->stream);
+  if (rc) return rc;
+  HBX_D2H(valid, dok, P);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+static int broadcast_decode_host(hbx_ctx* c, uint8_t* shards, const uint8_t* present, const uint8_t* leaf_hash,
+                                 const uint8_t* root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                                 uint8_t* out, uint64_t out_stride, uint64_t* out_len, int32_t* status,
+                                 const char* what) {
+  if (!c || !shards || !present || !root_expect || !out || !out_len || !status || inst == 0 || L == 0)
+    return fail(c, HBX_E_INVALID_ARG, "%s: bad args", what);
+  HIPCHK(c, hipSetDevice(c->device));
+  stream_scope ss_{c, pick(c, c->stream)};
+  const size_t n = (size_t)k + m, all = n * L * inst;
+  HBX_STAGE(d, 0, all, what);
+  HBX_STAGE(dp, 1, n * inst, what);
+  HBX_STAGE(dre, 2, (size_t)inst * 32, what);
+  HBX_STAGE(dout, 3, (size_t)inst * out_stride, what);
+  HBX_STAGE(dlen, 4, (size_t)inst * 12, what);  // out_len (u64) | status (i32)
+  uint8_t* dl = nullptr;
+  if (leaf_hash) {
+    dl = stage(c, 5, n * inst * 32);
+    if (!dl) return fail(c, HBX_E_OUT_OF_MEMORY, "%s: out of device memory (staging)", what);
+    HBX_H2D(dl, leaf_hash, n * inst * 32);
+  }
+  HBX_H2D(d, shards, all);
+  HBX_H2D(dp, present, n * inst);
+  HBX_H2D(dre, root_expect, (size_t)inst * 32);
+  int rc = broadcast_decode(c, d, dp, dl, dre, inst, k, m, L, dout, out_stride, (uint64_t*)dlen,
+                            (int32_t*)(dlen + (size_t)inst * 8), c->stream);
+  if (rc) return rc;
+  HBX_D2H(shards, d, all);
+  HBX_D2H(out, dout, (size_t)inst * out_stride);
+  HBX_D2H(out_len, dlen, (size_t)inst * 8);
+  HBX_D2H(status, dlen + (size_t)inst * 8, (size_t)inst * 4);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBX_OK;
+}
+
+int hbx_broadcast_decode(hbx_ctx* c, uint8_t* shards, const uint8_t* present, const uint8_t* root_expect, uint32_t inst,
+                         uint32_t k, uint32_t m, uint32_t L, uint8_t* out, uint64_t out_stride, uint64_t* out_len,
+                         int32_t* status) {
+  return broadcast_decode_host(c, shards, present, nullptr, root_expect, inst, k, m, L, out, out_stride, out_len,
+                               status, "hbx_broadcast_decode");
+}
+
+int hbx_broadcast_decode_leaves(hbx_ctx* c, uint8_t* shards, const uint8_t* present, const uint8_t* leaf_hash,
+                                const uint8_t* root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                                uint8_t* out, uint64_t out_stride, uint64_t* out_len, int32_t* status) {
+  if (!leaf_hash) return fail(c, HBX_E_INVALID_ARG, "hbx_broadcast_decode_leaves: leaf_hash is NULL");
+  return broadcast_decode_host(c, shards, present, leaf_hash, root_expect, inst, k, m, L, out, out_stride, out_len,
+                               status, "hbx_broadcast_decode_leaves");
+}
+#undef HBX_STAGE
+#undef HBX_H2D
+#undef HBX_D2H
+
 // ---- Common Coin ----------------------------------------------------------------------------
 // The true H = hash_g2(nonce) of the prepared nonces from H' = [m] H (k_h2_from_heff), once, on s.
 static int coin_true_h(hbx_ctx* c, hipStream_t s) {
@@ -1161,6 +1377,10 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
                        c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     c->coin_lines_ready = true;
+    // the lines are built on this call's stream: move the prepare event past them, so a later
+    // one-lane check on another stream (which waits on coin_ready_ev) is ordered after the build
+    if (!c->coin_ready_ev) HIPCHK(c, hipEventCreateWithFlags(&c->coin_ready_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->coin_ready_ev, s));
   }
   {
     timed t_(c, HBX_K_VERIFY_SIG, s);

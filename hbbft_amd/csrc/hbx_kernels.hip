@@ -446,13 +446,17 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
                                                       const line_block_d* __restrict__ lines,
                                                       const uint8_t* __restrict__ ct_ok, uint32_t n,
                                                       uint8_t* __restrict__ valid, uint32_t me,
-                                                      uint8_t* __restrict__ ct_valid, uint32_t fallback_only) {
+                                                      uint8_t* __restrict__ ct_valid, uint32_t fallback_only,
+                                                      uint32_t* __restrict__ fallback_lanes) {
   __shared__ uint32_t gslots[LDS_FQ12D_DWORDS * LDS_FQ12_STRIDE];  // final-exp base, one slot per lane
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j = blockIdx.y;
   if (i >= n) return;
   const size_t idx = (size_t)j * n + i;
-  if (fallback_only && valid[idx] != SHARE_FALLBACK) return;  // the lanes k_fe1 could not decide
+  if (fallback_only) {
+    if (valid[idx] != SHARE_FALLBACK) return;  // the lanes k_fe1 could not decide
+    if (fallback_lanes) atomicAdd(fallback_lanes, 1u);  // hbx_get_fallback_lanes
+  }
   const uint8_t res = share_precheck(s_status[idx], present == nullptr || present[idx] || i == me, i < n_keys,
                                      ct_ok[j] != 0);
   bool v = false;
@@ -578,7 +582,11 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   // takes the degenerate path, so the fallback check is exercised
   bool degenerate = STEP == 1 && force_fallback && (i % force_fallback) == 0;
   if (STEP == 0) {
-    fe1_step0<64, 64>(a, gf, gg);
+    if (fe1_step0<64, 64>(a, gf, gg)) {  // t = 1 after the easy part: the check holds (fe1d.hpp)
+      valid[idx] = HBX_SHARE_VALID;
+      if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : HBX_CT_VALID;
+      return;
+    }
   } else if (STEP == 1) {
     fe1_step_expmul<64, 64>(a, gt, gg, degenerate);
   } else if (STEP == 2) {

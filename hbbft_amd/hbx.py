@@ -76,9 +76,19 @@ EXPORTS = (
     "hbx_get_verify_lanes_used",
     "hbx_set_combine_lanes",
     "hbx_debug_force_fallback",
+    "hbx_get_fallback_lanes",
+    "hbx_build_id",
     "hbx_merkle_node_count",
     "hbx_merkle_build_d",
     "hbx_merkle_proofs_d",
+    "hbx_rs_encode",
+    "hbx_rs_reconstruct",
+    "hbx_merkle_roots",
+    "hbx_merkle_build",
+    "hbx_merkle_proofs",
+    "hbx_merkle_validate",
+    "hbx_broadcast_decode",
+    "hbx_broadcast_decode_leaves",
 )
 
 DIGEST_SHA256 = 0
@@ -137,6 +147,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_last_error.argtypes = [P]
     lib.hbx_last_error.restype = ctypes.c_char_p
     lib.hbx_version.restype = ctypes.c_char_p
+    lib.hbx_build_id.restype = ctypes.c_char_p
     lib.hbx_set_pk_shares.argtypes = [P, u8p, u32, i32p]
     lib.hbx_set_own_share.argtypes = [P, u32, u8p]
     lib.hbx_prepare_ciphertexts.argtypes = [P, u8p, u8p, u64p, u8p, u32, u8p]
@@ -175,14 +186,37 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.hbx_get_verify_lanes_used.argtypes = [P]
     lib.hbx_set_combine_lanes.argtypes = [P, ctypes.c_int]
     lib.hbx_debug_force_fallback.argtypes = [P, u32]
+    lib.hbx_get_fallback_lanes.argtypes = [P]
+    lib.hbx_get_fallback_lanes.restype = ctypes.c_int64
     lib.hbx_merkle_node_count.argtypes = [u32]
     lib.hbx_merkle_node_count.restype = u32
     lib.hbx_merkle_build_d.argtypes = [P, P, u32, u32, u32, P, P, P]
     lib.hbx_merkle_proofs_d.argtypes = [P, P, u32, P, u32, P, P, P, P, P, P]
+    # host-pointer Broadcast calls (numpy buffers; what a Rust FFI calls from Vec<u8>)
+    lib.hbx_rs_encode.argtypes = [P, P, u32, u32, u32, u32]
+    lib.hbx_rs_reconstruct.argtypes = [P, P, P, u32, u32, u32, u32, P]
+    lib.hbx_merkle_roots.argtypes = [P, P, u32, u32, u32, P]
+    lib.hbx_merkle_build.argtypes = [P, P, u32, u32, u32, P, P]
+    lib.hbx_merkle_proofs.argtypes = [P, P, u32, u32, P, u32, P, P, P, P, P]
+    lib.hbx_merkle_validate.argtypes = [P, P, u32, P, P, P, P, P, P, u32, u32, P]
+    lib.hbx_broadcast_decode.argtypes = [P, P, P, P, u32, u32, u32, u32, P, ctypes.c_uint64, P, P]
+    lib.hbx_broadcast_decode_leaves.argtypes = [P, P, P, P, P, u32, u32, u32, u32, P, ctypes.c_uint64, P, P]
     for name in ("hbx_get_share_status", "hbx_get_ct_status", "hbx_get_sig_share_status", "hbx_get_ct_hashes"):
         getattr(lib, name).argtypes = [P, u8p, ctypes.c_size_t]
     _lib = lib
     return lib
+
+
+def build_info() -> dict:
+    """Provenance of the loaded library: the source hash it was built from (hbx_build_id), the hash
+    of the sources in this tree (hbbft_amd/buildinfo.py) and whether they match."""
+    from . import buildinfo
+
+    lib = load_library()
+    built = lib.hbx_build_id().decode()
+    tree = buildinfo.source_hash()
+    return {"lib_source_sha256": built, "tree_source_sha256": tree, "match": built == tree,
+            "lib": os.path.relpath(LIB_PATH, buildinfo.ROOT)}
 
 
 def _u8(a: np.ndarray):
@@ -249,6 +283,13 @@ class Context:
         """hbx_debug_force_fallback (tests only): route every ``every``-th sender's one-lane check
         through the single-kernel fallback (0 = off)."""
         self._check(self.lib.hbx_debug_force_fallback(self.h, every))
+
+    def fallback_lanes(self) -> int:
+        """hbx_get_fallback_lanes: lanes of the last one-lane launch the fallback check decided."""
+        v = int(self.lib.hbx_get_fallback_lanes(self.h))
+        if v < 0:
+            self._check(v)
+        return v
 
     def set_combine_lanes(self, lanes: int):
         """hbx_set_combine_lanes: 0 auto (default), 1 (a lane per Lagrange term) or 4 (a quad per term)."""
@@ -539,6 +580,106 @@ class Context:
         self._check(self.lib.hbx_merkle_validate_d(
             self.h, d_values.data_ptr(), vlen, d_nodes.data_ptr(), d_sibs.data_ptr(), d_sides.data_ptr(),
             d_depth.data_ptr(), d_root.data_ptr(), d_sender.data_ptr(), count, nproofs, d_valid.data_ptr(), self._stream(stream)))
+
+    # -- Broadcast on host buffers (numpy; no device memory on the caller's side) ----------------
+    @staticmethod
+    def _host(a, dtype, shape=None, writable=False):
+        """A C-contiguous numpy array of `dtype` (and `shape`), in place when it already is one."""
+        if not isinstance(a, np.ndarray) or a.dtype != dtype or not a.flags["C_CONTIGUOUS"]:
+            if writable:
+                raise ValueError(f"need a C-contiguous {np.dtype(dtype)} numpy array (written in place)")
+            a = np.ascontiguousarray(a, dtype=dtype)
+        if shape is not None and tuple(a.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(a.shape)}")
+        return a
+
+    def rs_encode(self, shards: np.ndarray, k: int, m: int):
+        """hbx_rs_encode: shards uint8[inst, k + m, L] on the host, parity rows written in place."""
+        shards = self._host(shards, np.uint8, writable=True)
+        inst, n, L = shards.shape
+        assert n == k + m
+        self._check(self.lib.hbx_rs_encode(self.h, shards.ctypes.data, inst, k, m, L))
+
+    def rs_reconstruct(self, shards: np.ndarray, present, k: int, m: int) -> np.ndarray:
+        """hbx_rs_reconstruct: shards rebuilt in place; returns status int32[inst]."""
+        shards = self._host(shards, np.uint8, writable=True)
+        inst, n, L = shards.shape
+        pres = self._host(present, np.uint8, (inst, n))
+        st = np.zeros(inst, dtype=np.int32)
+        self._check(self.lib.hbx_rs_reconstruct(self.h, shards.ctypes.data, pres.ctypes.data, inst, k, m, L,
+                                                st.ctypes.data))
+        return st
+
+    def merkle_roots(self, shards) -> np.ndarray:
+        shards = self._host(shards, np.uint8)
+        inst, n, L = shards.shape
+        roots = np.zeros((inst, 32), dtype=np.uint8)
+        self._check(self.lib.hbx_merkle_roots(self.h, shards.ctypes.data, inst, n, L, roots.ctypes.data))
+        return roots
+
+    def merkle_build(self, shards):
+        """hbx_merkle_build -> (nodes uint8[inst, node_count(n), 32], roots uint8[inst, 32])."""
+        shards = self._host(shards, np.uint8)
+        inst, n, L = shards.shape
+        nodes = np.zeros((inst, self.merkle_node_count(n), 32), dtype=np.uint8)
+        roots = np.zeros((inst, 32), dtype=np.uint8)
+        self._check(self.lib.hbx_merkle_build(self.h, shards.ctypes.data, inst, n, L, nodes.ctypes.data,
+                                              roots.ctypes.data))
+        return nodes, roots
+
+    def merkle_proofs(self, nodes, n: int, req):
+        """hbx_merkle_proofs: req uint32[count, 2] = (instance, leaf) -> (node_hash, sib_hash, sides,
+        depth, root) as hbx_merkle_validate takes them."""
+        nodes = self._host(nodes, np.uint8)
+        inst = nodes.shape[0]
+        req = self._host(req, np.uint32)
+        count = req.shape[0]
+        nh = np.zeros((count, 17, 32), dtype=np.uint8)
+        sh = np.zeros((count, 16, 32), dtype=np.uint8)
+        sides = np.zeros(count, dtype=np.uint32)
+        depth = np.zeros(count, dtype=np.uint32)
+        root = np.zeros((count, 32), dtype=np.uint8)
+        self._check(self.lib.hbx_merkle_proofs(self.h, nodes.ctypes.data, inst, n, req.ctypes.data, count,
+                                               nh.ctypes.data, sh.ctypes.data, sides.ctypes.data, depth.ctypes.data,
+                                               root.ctypes.data))
+        return nh, sh, sides, depth, root
+
+    def merkle_validate(self, values, nodes, sibs, sides, depth, root, sender, count: int) -> np.ndarray:
+        """hbx_merkle_validate: returns valid uint8[nproofs]."""
+        values = self._host(values, np.uint8)
+        nproofs, vlen = values.shape
+        args = [self._host(nodes, np.uint8, (nproofs, 17, 32)), self._host(sibs, np.uint8, (nproofs, 16, 32)),
+                self._host(sides, np.uint32, (nproofs,)), self._host(depth, np.uint32, (nproofs,)),
+                self._host(root, np.uint8, (nproofs, 32)), self._host(sender, np.uint32, (nproofs,))]
+        valid = np.zeros(nproofs, dtype=np.uint8)
+        self._check(self.lib.hbx_merkle_validate(self.h, values.ctypes.data, vlen, *[a.ctypes.data for a in args],
+                                                 count, nproofs, valid.ctypes.data))
+        return valid
+
+    def broadcast_decode(self, shards, present, root, k: int, m: int, leaf_hash=None):
+        """hbx_broadcast_decode[_leaves]: shards rebuilt in place -> (out uint8[inst, k L], out_len
+        uint64[inst], status int32[inst])."""
+        shards = self._host(shards, np.uint8, writable=True)
+        inst, n, L = shards.shape
+        if n != k + m:
+            raise ValueError(f"broadcast_decode: {n} shards per instance != k + m = {k + m}")
+        pres = self._host(present, np.uint8, (inst, n))
+        root = self._host(root, np.uint8, (inst, 32))
+        stride = max(k * L, 1)
+        out = np.zeros((inst, stride), dtype=np.uint8)
+        out_len = np.zeros(inst, dtype=np.uint64)
+        st = np.zeros(inst, dtype=np.int32)
+        if leaf_hash is None:
+            self._check(self.lib.hbx_broadcast_decode(self.h, shards.ctypes.data, pres.ctypes.data, root.ctypes.data,
+                                                      inst, k, m, L, out.ctypes.data, stride, out_len.ctypes.data,
+                                                      st.ctypes.data))
+        else:
+            lh = self._host(leaf_hash, np.uint8, (inst, n, 32))
+            self._check(self.lib.hbx_broadcast_decode_leaves(self.h, shards.ctypes.data, pres.ctypes.data,
+                                                             lh.ctypes.data, root.ctypes.data, inst, k, m, L,
+                                                             out.ctypes.data, stride, out_len.ctypes.data,
+                                                             st.ctypes.data))
+        return out, out_len, st
 
     def merkle_node_count(self, n: int) -> int:
         return int(self.lib.hbx_merkle_node_count(n))

@@ -5,9 +5,10 @@ proposer column: rank g owns a contiguous block of proposers together with their
 hoisted hashes, prepared lines and combines; key material is replicated.  Nothing crosses GPUs
 while the kernels run.  Afterwards ONE all-gather (RCCL over xGMI on GPUs, gloo in the CPU tests)
 assembles every rank's fixed-size result slab -- per-share HBX_SHARE_* status bytes, per-ciphertext
-HBX_CT_* bytes, per-proposer combine status -- so each rank holds the node's complete epoch result,
-the input the reference's fault-log and decryption logic consumes (honey_badger.rs:422-461,
-:315-349; hbbft_amd/honey_badger.py).  Plaintexts stay on the GPU that decrypted them.
+HBX_CT_* bytes, per-proposer combine status and the decrypted plaintexts (the rank's decryption
+output buffer is the slab's plaintext region, so gathering them costs no copy) -- so each rank holds
+the node's complete epoch result and every contribution, the input the reference's fault-log and
+decryption logic consumes (honey_badger.rs:422-461, :315-349; hbbft_amd/honey_badger.py).
 """
 from __future__ import annotations
 

@@ -104,6 +104,10 @@ int hbx_ctx_destroy(hbx_ctx* ctx);
 const char* hbx_last_error(const hbx_ctx* ctx);
 /* Library version string, e.g. "hbx 0.1.0 gfx950". */
 const char* hbx_version(void);
+/* SHA-256 (hex) of the sources this library was built from (hbbft_amd/buildinfo.py source_hash,
+ * set by tools/build.py); "unknown" for a build outside it.  Provenance only: no reference
+ * counterpart. */
+const char* hbx_build_id(void);
 
 /* Kernel timing (instrumentation; no reference counterpart).  With timing on, the library
  * brackets each launch of the kernels below with HIP events recorded on the stream the kernel
@@ -147,8 +151,15 @@ int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
 /* Tests only: in one-lane checks, treat the lane of every `every`-th sender (0 = none, the default)
  * as if its compressed squarings had met a zero denominator, so the single-kernel fallback check
- * decides it (a path real inputs reach with probability ~2^-760).  Results are unchanged. */
+ * decides it.  Results are unchanged.  (Real inputs reach that path only through an element with a
+ * zero Fq2 coefficient at the end of a compressed run, ~2^-760 for values nobody chose; the one
+ * degenerate start a proposer can choose -- a ciphertext with r = 3(x^2 - 1), for which every honest
+ * share's check is 1 after the easy part -- is decided by the first step without a fallback.) */
 int hbx_debug_force_fallback(hbx_ctx* ctx, uint32_t every);
+/* Lanes of the last one-lane decryption-share launch that the single-kernel fallback check decided
+ * (0 unless hbx_debug_force_fallback is on); waits for the launch.  Diagnostics: no reference
+ * counterpart. */
+int64_t hbx_get_fallback_lanes(hbx_ctx* ctx);
 /* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
  * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over
  * one-wave blocks (k_combine_q, t <= 128), 0 = by launch size (default: 4 when the quad blocks fit
@@ -414,6 +425,47 @@ int hbx_broadcast_decode_leaves_d(hbx_ctx* ctx, uint8_t* d_shards, const uint8_t
                                   const uint8_t* d_leaf_hash, const uint8_t* d_root_expect, uint32_t inst,
                                   uint32_t k, uint32_t m, uint32_t L, uint8_t* d_out, uint64_t out_stride,
                                   uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Host-pointer forms of the Broadcast calls: the same operations and layouts on HOST buffers,
+ * staged through device buffers the context owns, on the context's own stream; they block until
+ * the outputs are back (the stack-A/B convention above).  What a thin Rust FFI calls from
+ * Vec<u8> / &[u8] without a HIP runtime binding of its own:
+ *   hbx_rs_encode          Coding::encode / ReedSolomon::encode (src/broadcast.rs:632-640, called at
+ *                          :366): shards[inst][k + m][L]; reads the k data rows, writes the m parity
+ *                          rows of every instance.
+ *   hbx_rs_reconstruct     Coding::reconstruct_shards (src/broadcast.rs:643-657, called at :667):
+ *                          present[inst][k + m] bytes; shards rewritten in place, status[inst].
+ *   hbx_merkle_roots       MerkleTree::from_vec(..).root_hash() (src/broadcast.rs:381): roots[inst][32].
+ *   hbx_merkle_build       the whole tree (src/broadcast.rs:381): nodes[inst][hbx_merkle_node_count(n)][32],
+ *                          roots optional.
+ *   hbx_merkle_proofs      MerkleTree::gen_proof (src/broadcast.rs:389-401) from hbx_merkle_build's
+ *                          nodes of `inst` instances: req[count][2] = (instance, leaf); outputs as
+ *                          hbx_merkle_proofs_d, sides[count] and depth[count] as uint32.
+ *   hbx_merkle_validate    Broadcast::validate_proof (src/broadcast.rs:555-575, called for Value at
+ *                          :430 and Echo at :451); arrays as hbx_merkle_validate_d, valid[nproofs].
+ *   hbx_broadcast_decode   decode_from_shards + glue_shards (src/broadcast.rs:660-707): shards
+ *                          rewritten in place (reconstructed rows), out[inst][out_stride],
+ *                          out_len[inst], status[inst].
+ *   hbx_broadcast_decode_leaves  the same with the validated Echo proofs' leaf digests
+ *                          (leaf_hash[inst][k + m][32]). */
+int hbx_rs_encode(hbx_ctx* ctx, uint8_t* shards, uint32_t inst, uint32_t k, uint32_t m, uint32_t L);
+int hbx_rs_reconstruct(hbx_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t inst, uint32_t k, uint32_t m,
+                       uint32_t L, int32_t* status);
+int hbx_merkle_roots(hbx_ctx* ctx, const uint8_t* shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* roots);
+int hbx_merkle_build(hbx_ctx* ctx, const uint8_t* shards, uint32_t inst, uint32_t n, uint32_t L, uint8_t* nodes,
+                     uint8_t* roots);
+int hbx_merkle_proofs(hbx_ctx* ctx, const uint8_t* nodes, uint32_t inst, uint32_t n, const uint32_t* req,
+                      uint32_t count, uint8_t* node_hash, uint8_t* sib_hash, uint32_t* sides, uint32_t* depth,
+                      uint8_t* root);
+int hbx_merkle_validate(hbx_ctx* ctx, const uint8_t* values, uint32_t vlen, const uint8_t* node_hash,
+                        const uint8_t* sib_hash, const uint32_t* sides, const uint32_t* depth, const uint8_t* root,
+                        const uint32_t* sender, uint32_t count, uint32_t nproofs, uint8_t* valid);
+int hbx_broadcast_decode(hbx_ctx* ctx, uint8_t* shards, const uint8_t* present, const uint8_t* root_expect,
+                         uint32_t inst, uint32_t k, uint32_t m, uint32_t L, uint8_t* out, uint64_t out_stride,
+                         uint64_t* out_len, int32_t* status);
+int hbx_broadcast_decode_leaves(hbx_ctx* ctx, uint8_t* shards, const uint8_t* present, const uint8_t* leaf_hash,
+                                const uint8_t* root_expect, uint32_t inst, uint32_t k, uint32_t m, uint32_t L,
+                                uint8_t* out, uint64_t out_stride, uint64_t* out_len, int32_t* status);
 
 #ifdef __cplusplus
 }

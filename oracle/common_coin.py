@@ -9,7 +9,9 @@ messages and outputs, in the same order:
 
 * ``input``            common_coin.rs:90-97 -- once: ``had_input``; ``get_coin`` (:138-147): a
   validator signs the nonce (``SecretKeyShare::sign``, :142), sends the share to all and handles
-  it as its own message (``handle_share``); a non-validator goes straight to ``try_output``;
+  it as its own message (``handle_share``) -- unless that returns an error, which drops the step
+  and with it the message (``?`` at :145; the error is filed under ``None``); a non-validator goes
+  straight to ``try_output``;
 * ``handle_message``   :100-110 -- ignored once ``terminated`` (no fault even for a bad share);
 * ``handle_share``     :149-161 -- unknown sender -> ``Err(UnknownSender)``; a share that does not
   verify (``PublicKeyShare::verify``, :151) -> fault ``UnverifiedSignatureShareSender`` and NO
@@ -112,19 +114,26 @@ class CoinNode:
             self._try_output(inst, None)
             return
         share = self._sign(coin)
-        self.sent.append((inst, share))
-        self._handle_share(inst, self.me, share)
+        # get_coin (:142-146) builds the Target::All message, then `step.extend(self.handle_share(..)?)`:
+        # an Err from our own share's try_output drops the whole step, message included -- the share
+        # is never sent, and had_input stays set, so it never will be
+        n_err = len(self.errors)
+        self._handle_share(inst, self.me, share, who=None)
+        if len(self.errors) == n_err:
+            self.sent.append((inst, share))
 
-    def _handle_share(self, inst: int, sender: int, share):
+    def _handle_share(self, inst: int, sender: int, share, who=-1):
+        """``who``: whose call returns an error (-1: the message's sender; None: our own input)."""
+        who = sender if who == -1 else who
         coin = self.coins[inst]
         if not 0 <= sender < self.n:
-            self.errors.append((sender, UNKNOWN_SENDER))
+            self.errors.append((who, UNKNOWN_SENDER))
             return
         if not self._verify(sender, share, coin):
             self.faults.append((sender, UNVERIFIED_SIGNATURE_SHARE_SENDER))
             return
         coin.received[sender] = share
-        self._try_output(inst, sender)
+        self._try_output(inst, who)
 
     def _try_output(self, inst: int, who):
         """``who``: the sender of the message being handled (None: our own input), whose

@@ -56,3 +56,14 @@ def test_shard_layout():
         shard.proposer_range(10, 4, 4)
     lay = shard.slab_layout(256, 32)
     assert lay["size"] == 256 * 32 + 32 + 128
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built")
+def test_library_was_built_from_these_sources():
+    """Provenance: the shipped library carries the SHA-256 of the sources it was
+    built from (hbx_build_id, compiled in by tools/build.py); it must be this tree's."""
+    from hbbft_amd import buildinfo
+
+    lib = ctypes.CDLL(LIB)
+    lib.hbx_build_id.restype = ctypes.c_char_p
+    assert lib.hbx_build_id().decode() == buildinfo.source_hash()

@@ -73,7 +73,14 @@ def test_replay_retries_a_failed_combination():
 
     node = Node(n, me, pks, sks.secret_key_share(me), ns).run(events)
     check_against_oracle(res, node)
-    assert (None, oc.VERIFICATION_FAILED) in node.errors or any(e == oc.VERIFICATION_FAILED for _, e in node.errors)
+    # instance 0's threshold is crossed by our own share at input time: the failed combination is
+    # our input call's error, and get_coin's `?` (common_coin.rs:145) drops the step with our
+    # outgoing share -- it is never sent (had_input stays set)
+    assert (None, oc.VERIFICATION_FAILED) in node.errors
+    assert 0 not in {inst for inst, _ in node.sent}
+    assert 0 not in {inst for inst, _ in res.sent}
+    assert {inst for inst, _ in node.sent} == {inst for inst, _ in res.sent} != set()
+    assert 0 in {inst for inst, _ in node.outputs}  # retried on the next share, then output
     assert res.engine_combines == 2
 
 

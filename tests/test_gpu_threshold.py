@@ -343,6 +343,7 @@ def test_one_lane_fallback_path_matches_golden(hbx_ctx, name):
     hbx_ctx.debug_force_fallback(3)
     try:
         _device_epoch(hbx_ctx, d, own=False)
+        assert hbx_ctx.fallback_lanes() > 0  # the forced lanes did take the fallback check
         hbx_ctx.set_own_share(int(d["own_me"]), d["own_sk"].tobytes())
         try:
             _device_epoch(hbx_ctx, d, own=True)
@@ -350,4 +351,60 @@ def test_one_lane_fallback_path_matches_golden(hbx_ctx, name):
             hbx_ctx.set_own_share(0, None)
     finally:
         hbx_ctx.debug_force_fallback(0)
+        hbx_ctx.set_verify_lanes(0)
+
+
+def degenerate_epoch():
+    """Two ciphertexts at N = 4 (oracle crypto), the first built with r = m = 3(x^2 - 1) mod r: then
+    W = [m] H = H' and every honest share is S_i = [m] pk_i, so both Miller pairs of a check use
+    H''s lines at P and -P, f lies in Fq6 and the easy part of the final exponentiation gives 1
+    (the compressed squarings would start at g3 = 0).  One share of each ciphertext is
+    another sender's (invalid)."""
+    from oracle import bls12_381 as bls
+    from oracle import threshold as tc
+    from oracle.chacha_rand04 import ChaChaRng04
+
+    n = 4
+    sks = tc.SecretKeySet.random(1, ChaChaRng04([0x68626278, 0x72656D, 5]))
+    pks = sks.public_keys()
+    m = 3 * (bls.BLS_X ** 2 - 1) % bls.R
+    cts = [tc.encrypt(pks.public_key(), msg, r) for msg, r in ((b"r = 3(x^2 - 1)", m), (b"any other r", 0x1234567))]
+    shares = np.zeros((2, n, 48), dtype=np.uint8)
+    expect = np.ones((2, n), dtype=bool)
+    for j, ct in enumerate(cts):
+        for i in range(n):
+            src = (i + 1) % n if i == 2 else i
+            shares[j, i] = np.frombuffer(bls.g1_compress(tc.decrypt_share(sks.secret_key_share(src), ct)), np.uint8)
+        expect[j, 2] = False
+    wire = [(bls.g1_compress(u), v, bls.g2_compress(w)) for u, v, w in cts]
+    pk_comp = [bls.g1_compress(pks.public_key_share(i)) for i in range(n)]
+    return sks, pks, cts, wire, pk_comp, shares, expect
+
+
+@pytest.mark.gpu
+def test_degenerate_ciphertext_r_m(hbx_ctx):
+    """A ciphertext with r = 3(x^2 - 1) (degenerate_epoch): its honest shares verify, the forged
+    one does not, and no one-lane check is sent to the fallback (k_fe1<0> decides t = 1); the
+    own-share lane gives Ciphertext::verify = valid.  Lanes 1 (steps), 7 (single kernel), 6, 3."""
+    _, _, _, wire, pk_comp, shares, expect = degenerate_epoch()
+    sks = degenerate_epoch()[0]
+    assert (hbx_ctx.set_pk_shares(pk_comp) == 0).all()
+    try:
+        for lanes in (1, 7, 6, 3):
+            hbx_ctx.set_verify_lanes(lanes)
+            assert hbx_ctx.prepare_ciphertexts(wire).all()
+            np.testing.assert_array_equal(hbx_ctx.verify_dec_shares(shares), expect)
+            assert hbx_ctx.verify_lanes_used() == lanes
+            if lanes == 1:
+                assert hbx_ctx.fallback_lanes() == 0
+        hbx_ctx.set_verify_lanes(1)
+        hbx_ctx.set_own_share(1, sks.secret_key_share(1).to_bytes(32, "big"))
+        try:
+            assert hbx_ctx.prepare_ciphertexts(wire).all()
+            np.testing.assert_array_equal(hbx_ctx.verify_dec_shares(shares), expect)
+            assert hbx_ctx.fallback_lanes() == 0
+            np.testing.assert_array_equal(hbx_ctx.ct_status(2), [1, 1])
+        finally:
+            hbx_ctx.set_own_share(0, None)
+    finally:
         hbx_ctx.set_verify_lanes(0)

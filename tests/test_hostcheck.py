@@ -183,6 +183,23 @@ def test_fe1_chain_matches_final_exponentiation(hc):
         assert hc.hc_fe1_chain_cmp(pa, qa, ng1, qb) == (7 if trial % 2 == 0 else 3)
 
 
+def test_fe1_step0_decides_t_one(hc):
+    """a ciphertext with r = m = 3(x^2 - 1) makes W = H' and every honest share [m] pk_i,
+    so the check's two Miller pairs are H''s lines at P and -P and t = 1 after the easy part; the
+    compressed squarings of the chain would then all meet g3 = 0 (the fallback).  fe1_step0 reports
+    t = 1 (k_fe1<0> decides the share valid there); an ordinary valid check is not t = 1."""
+    m = 3 * (bls.BLS_X ** 2 - 1) % bls.R
+    pk_m = bls.g1_mul(bls.G1_GEN, 0x5eed * m % bls.R)
+    hp = bls.g2_compress(bls.g2_mul(bls.G2_GEN, 0xbeef))
+    r = hc.hc_fe1_step0_one(bls.g1_compress(pk_m), hp, bls.g1_compress(bls.g1_neg(pk_m)), hp)
+    assert r & 1 and r & 2  # t = 1, and the runs would degenerate
+    a = 0x1234
+    q = bls.g2_mul(bls.G2_GEN, 0x777)
+    r = hc.hc_fe1_step0_one(bls.g1_compress(bls.g1_mul(bls.G1_GEN, a)), bls.g2_compress(q),
+                            bls.g1_compress(bls.g1_neg(bls.G1_GEN)), bls.g2_compress(bls.g2_mul(q, a)))
+    assert r == 4  # holds, decided by the whole chain
+
+
 def test_sha256_and_hash_g1_g2(hc):
     for n in (0, 1, 55, 56, 64, 65, 200):
         m = bytes(range(n % 251))[:n] + bytes(max(0, n - 251))

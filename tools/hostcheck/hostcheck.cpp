@@ -166,6 +166,35 @@ int hc_fe1_chain_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, co
   const bool v1 = fq12_is_one(e1), v2 = fq12d_is_one_seq(e2d);
   return same + 2 * (v1 == v2 ? 1 : 0) + 4 * (v2 ? 1 : 0);
 }
+// k_fe1<0>'s early decision: bit 0 = step 0 found t = 1, bit 1 = the rest of the chain would have met
+// a degenerate compressed run (g3 = 0), bit 2 = the chain's verdict is 1
+int hc_fe1_step0_one(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
+  g1a PA, PB; g2a QA, QB;
+  if (g1_decompress(pa, PA) != HBX_PT_OK || g1_decompress(pb, PB) != HBX_PT_OK) return -1;
+  if (g2_decompress(qa, QA) != HBX_PT_OK || g2_decompress(qb, QB) != HBX_PT_OK) return -2;
+  static line_pre LA[MILLER_LINES], LB[MILLER_LINES];
+  static line_pre_d DA[MILLER_LINES], DB[MILLER_LINES];
+  static fq2 scratch[2 * MILLER_LINES];
+  g2_prepare_lines(QA, LA, scratch);
+  g2_prepare_lines(QB, LB, scratch);
+  for (int i = 0; i < MILLER_LINES; i++) {
+    DA[i] = line_to_d(LA[i]);
+    DB[i] = line_to_d(LB[i]);
+  }
+  const fq12d fd = miller_loop2_d(DA, fqd_from_fq(PA.x), fqd_from_fq(PA.y), true, DB, fqd_from_fq(PB.x),
+                                  fqd_from_fq(PB.y), true);
+  static uint32_t a[FE1_WORDS], gf[FE1_WORDS], gt[FE1_WORDS], gg[FE1_WORDS];
+  s1_put_fq12d<1>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
+  const bool one = fe1_step0<1, 1>(a, gf, gg);
+  bool degenerate = false;
+  fe1_step_expmul<1, 1>(a, gt, gg, degenerate);
+  fe1_step_expmul<1, 1>(a, (uint32_t*)nullptr, gg, degenerate);
+  fe1_step3<1, 1>(a, gf, gg, degenerate);
+  fe1_step4<1, 1>(a, gf, gt);
+  fe1_step5<1, 1>(a, gf, gg, degenerate);
+  const bool v = fq12d_is_one_seq(fe1_step6<1, 1>(a, gt, gg, degenerate));
+  return (one ? 1 : 0) + (degenerate ? 2 : 0) + (v ? 4 : 0);
+}
 // digit-form product against the 12-limb one on canonical inputs: out = canonical a b (BE)
 void hc_fqd_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   const fqd x = fqd_from_fq(fq_to_mont(fq_from_be(a))), y = fqd_from_fq(fq_to_mont(fq_from_be(b)));

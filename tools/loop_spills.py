@@ -20,6 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import isa_check  # noqa: E402
 
 VERBOSE = "-v" in sys.argv
+MIX = "-m" in sys.argv  # instruction mix of every loop body of 300+ instructions
 ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
 TARGET = re.compile(r"<[^+>]+\+0x([0-9a-f]+)>")
 
@@ -74,6 +75,24 @@ def analyse(disasm: str):
             for (a, b), c in sorted(inner.items()):
                 n_in = sum(1 for x, _ in body if a <= x <= b)
                 print(f"    loop {a:#x}..{b:#x} ({n_in} insts): {c} scratch ops")
+        if MIX:
+            for a, b in sorted(set(loops)):
+                ops = [ins.split()[0] for x, ins in body if a <= x <= b]
+                if len(ops) < 300:
+                    continue
+                mad = sum(o.startswith("v_mad_") for o in ops)
+                valu = sum(o.startswith("v_") for o in ops)
+                sc = sum(o.startswith(("scratch_", "buffer_")) for o in ops)
+                ds = sum(o.startswith("ds_") for o in ops)
+                nop = sum(o == "s_nop" for o in ops)
+                acc = sum(o.startswith("v_accvgpr") for o in ops)
+                top = {}
+                for o in ops:
+                    if o.startswith("v_") and not o.startswith("v_mad_"):
+                        top[o] = top.get(o, 0) + 1
+                top = sorted(top.items(), key=lambda kv: -kv[1])[:10]
+                print(f"  {name[:40]} loop {a:#x}..{b:#x}: {len(ops)} insts, v_mad {mad}, other VALU {valu - mad} "
+                      f"(accvgpr moves {acc}), scratch {sc}, ds {ds}, s_nop {nop}; {top}")
         out.append((name, len(body), total, in_loop, loop_insts, len(loops)))
     return out
 
@@ -108,5 +127,5 @@ def main(path):
 
 if __name__ == "__main__":
     for p in sys.argv[1:]:
-        if p != "-v":
+        if p not in ("-v", "-m"):
             main(p)
