@@ -1033,32 +1033,38 @@ def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
 # ----------------------------------------------------------------------------------------------
 # Stacks B and C across GPUs: instance sharding + one all-gather of result slabs
 # ----------------------------------------------------------------------------------------------
+def _sync(torch, dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def _timed_steps(torch, dist, dev, world, steps, fn):
-    """Barrier + synchronize on both sides of ``steps`` calls of fn; max over ranks (seconds)."""
+    """Barrier + synchronize on both sides of ``steps`` calls of fn; max over ranks (seconds).
+    (``dev`` may be the CPU: tests/test_bench_shard_legs.py runs the legs over gloo.)"""
     fn()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     dist.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     dist.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
 
 
-def sharded_c4(args, dev, torch, Context, world, rank):
+def sharded_c4(args, dev, torch, Context, world, rank, n=128, inst=256):
     """C4 across ``world`` GPUs: rank g owns instances instance_range(256, world, g) -- their nonces,
     the 128 signature shares of each, the combines; one all-gather of (share status, signature,
-    combine status, master-ok, parity) slabs gives every rank the round's result."""
+    combine status, master-ok, parity) slabs gives every rank the round's result.  (``n`` / ``inst``
+    smaller and ``Context`` a stand-in: the CPU gloo test of this leg's control flow.)"""
     import torch.distributed as dist
 
     from hbbft_amd import netinfo, shard
 
-    n, inst = 128, 256
     lo, hi = shard.instance_range(inst, world, rank)
     c = hi - lo
     lay = shard.coin_layout(inst, n, world)
@@ -1099,17 +1105,17 @@ def sharded_c4(args, dev, torch, Context, world, rank):
             "ms_per_round": round(el / steps * 1e3, 3), "instances_per_gpu": c, "scaling": "strong"}
 
 
-def sharded_c5(args, dev, torch, Context, world, rank):
+def sharded_c5(args, dev, torch, Context, world, rank, n=128, inst=128, plen=1 << 20):
     """C5 across ``world`` GPUs: rank g owns proposals instance_range(128, world, g): encode, SHA-256
     Merkle roots and the decode with the last 42 shards missing; one all-gather of (root, decode
-    status, output length) slabs; payloads stay on the owning GPU."""
+    status, output length) slabs; payloads stay on the owning GPU.  (Smaller shapes and a stand-in
+    ``Context``: the CPU gloo test of this leg.)"""
     import torch.distributed as dist
 
     from hbbft_amd import shard
 
-    n, f = 128, 42
+    f = (n - 1) // 3
     k, m = n - 2 * f, 2 * f
-    inst, plen = 128, 1 << 20
     L = (plen + 4 + k - 1) // k
     lo, hi = shard.instance_range(inst, world, rank)
     c = hi - lo
@@ -1145,7 +1151,7 @@ def sharded_c5(args, dev, torch, Context, world, rank):
         full = shard.assemble_fields(gathered[0].cpu().numpy(), lay, inst, world)
         assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "decoded payload"
     assert (full["decode_status"] == 0).all() and (full["out_len"] == plen).all(), "gathered decodes"
-    return {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} 1 MiB proposals sharded by instance over {world} "
+    return {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} {plen} B proposals sharded by instance over {world} "
                         f"GPUs (encode + SHA-256 roots + decode, + one all-gather of {lay.size} B slabs)",
             "value": round(inst * plen * steps / el / 1e9, 2), "unit": "GB/s of proposals (whole job, wall)",
             "ms_per_round": round(el / steps * 1e3, 3), "instances_per_gpu": c, "scaling": "strong"}

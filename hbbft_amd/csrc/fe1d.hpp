@@ -198,7 +198,14 @@ HBX_HD fq12d fq12d_mul_slot(const fq12d& X, P y) {
 #else
 #define HBX_CYC_SEQ1() ((void)0)
 #endif
+#ifndef HBX_FE1_LAZY
+#define HBX_FE1_LAZY 1  // 1: Fq4 squarings by fq4d_sqr_lazy (one reduction per output coordinate)
+#endif
 HBX_HD void fq4d_sqr_seq(const fq2d& a, const fq2d& b, fq2d& c0, fq2d& c1) {
+#if HBX_FE1_LAZY
+  fq4d_sqr_lazy(a, b, c0, c1);
+  HBX_CYC_SEQ1();
+#else
   const fq2d t0 = fq2d_sqr(a);
   HBX_CYC_SEQ2();
   const fq2d t1 = fq2d_sqr(b);
@@ -206,6 +213,7 @@ HBX_HD void fq4d_sqr_seq(const fq2d& a, const fq2d& b, fq2d& c0, fq2d& c1) {
   c0 = fq2d_norm(fq2d_add(fq2d_mul_xi(t1), t0));
   c1 = fq2d_norm(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_add(a, b)), t0), t1));
   HBX_CYC_SEQ1();
+#endif
 }
 HBX_HD fq12d fq12d_cyclotomic_sqr_seq(const fq12d& f) {
   fq2d z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
@@ -246,6 +254,20 @@ HBX_HD fq2d fq2d_lin(const fq2d& a3, const fq2d& b2, bool minus) {  // reduce(3 
   return fq2d_reduce(minus ? fq2d_sub(a, b) : fq2d_add(a, b));
 }
 HBX_HD void karabina_sqr(fq12c& c) {
+#if HBX_FE1_LAZY
+  // (g3 + g2 Y)^2 = (g3^2 + xi g2^2) + 2 g2 g3 Y and (g1 + g5 Y)^2 = (g1^2 + xi g5^2) + 2 g1 g5 Y:
+  // the six squarings as two lazily reduced Fq4 squarings (fieldd.hpp fq4d_sqr_lazy)
+  fq2d p1, x23, p2, x15;
+  fq4d_sqr_lazy(c.g3, c.g2, p1, x23);
+  HBX_SEQ();
+  fq4d_sqr_lazy(c.g1, c.g5, p2, x15);
+  HBX_SEQ();
+  const fq2d n1 = fq2d_lin(p1, c.g1, true);
+  const fq2d n2 = fq2d_lin(p2, c.g2, true);
+  const fq2d n3 = fq2d_lin(fq2d_norm(fq2d_mul_xi(x15)), c.g3, false);
+  const fq2d n5 = fq2d_lin(x23, c.g5, false);
+  c = fq12c{n1, n2, n3, n5};
+#else
   const fq2d s1 = fq2d_sqr(c.g1);
   HBX_SEQ();
   const fq2d s5 = fq2d_sqr(c.g5);
@@ -263,6 +285,7 @@ HBX_HD void karabina_sqr(fq12c& c) {
   const fq2d n3 = fq2d_lin(fq2d_norm(fq2d_mul_xi(x15)), c.g3, false);
   const fq2d n5 = fq2d_lin(x23, c.g5, false);
   c = fq12c{n1, n2, n3, n5};
+#endif
 }
 // decompressed element (reduced); `degenerate` set when g3 = 0
 HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
@@ -435,35 +458,72 @@ template <int SG, class PG>
 HBX_HD fq6d s1_get_half(PG p, int h) {
   return fq6d{s1_get_fq2d<SG>(p, 3 * h), s1_get_fq2d<SG>(p, 3 * h + 1), s1_get_fq2d<SG>(p, 3 * h + 2)};
 }
-// fe1_easy_first restated over the slots, so that f never sits in registers beside the products
-// (it held f, g and the accumulators at once: 718 VGPRs spilled): N(f) from f's halves one at a
-// time, N^-1 into slot a, g = conj(f)^2 parked in slot G (overwritten at the end), each half of
-// g times N^-1 streamed from a.
+// fe1_easy_first restated over the slots with at most two Fq6 values in registers at a time (the
+// round-4 version held f's halves beside an Fq12 squaring: 224 spilled VGPRs, 0.46 GB of scratch
+// traffic per N=256 launch).  With A = f0^2, B = v f1^2, C = f0 f1 (three Fq6 products, each
+// streaming its second operand from slot F): N(f) = A - B, conj(f)^2 = (A + B) - 2 C w, and
+// t0 = conj(f)^2 / N(f) -- three Fq6 products for N(f) and conj(f)^2 instead of four.  Slot a
+// holds v f1^2 (words 78..155), then N^-1 (words 0..77); slot G's half 0 holds A + B until t0's
+// first half is formed.
 template <int S, int SG, class P, class PG>
 HBX_HD bool fe1_step0(P a, PG gf, PG gg) {
   {
-    fq6d n;
-    {
-      const fq6d f0 = s1_get_half<SG>(gf, 0);
-      n = fq6d_mul(f0, f0);
-    }
-    HBX_SEQ();
+    // B = v f1^2 -> slot a words 78..155
+    fq6d B = fq6d_zero_();
     {
       const fq6d f1 = s1_get_half<SG>(gf, 1);
-      n = fq6d_reduce(fq6d_sub(n, fq6d_mul_v(fq6d_mul(f1, f1))));
+      fq6d_mul_acc1(B, f1, [&](int q) { return s1_get_fq2d<SG>(gf, 3 + q); });
+    }
+    B = fq6d_norm(fq6d_mul_v(B));
+    s1_put_fq2d<S>(a, 3, B.c0);
+    s1_put_fq2d<S>(a, 4, B.c1);
+    s1_put_fq2d<S>(a, 5, B.c2);
+  }
+  HBX_SEQ();
+  {
+    // A = f0^2; N = A - B (kept), A + B -> slot G half 0
+    fq6d A = fq6d_zero_();
+    {
+      const fq6d f0 = s1_get_half<SG>(gf, 0);
+      fq6d_mul_acc1(A, f0, [&](int q) { return s1_get_fq2d<SG>(gf, q); });
+    }
+    HBX_SEQ();
+    fq6d n;
+#pragma unroll 1
+    for (int q = 0; q < 3; q++) {  // one Fq2 coefficient at a time (B from the slot)
+      const fq2d b = s1_get_fq2d<S>(a, 3 + q);
+      const fq2d aq = q == 0 ? A.c0 : q == 1 ? A.c1 : A.c2;
+      s1_put_fq2d<SG>(gg, q, fq2d_reduce(fq2d_add(aq, b)));
+      const fq2d nq = fq2d_reduce(fq2d_sub(aq, b));
+      if (q == 0) n.c0 = nq;
+      else if (q == 1) n.c1 = nq;
+      else n.c2 = nq;
     }
     HBX_SEQ();
     fq6d_inv_to_slot<S>(n, a);  // words [0, 78): N^-1
   }
   HBX_SEQ();
-  s1_put_fq12d<SG>(gg, fq12d_sqr(fq12d_conj(s1_get_fq12d<SG>(gf))));  // g
+  fq12d r;
+  {
+    // t0.c1 = -2 C N^-1, C = f0 f1
+    fq6d C = fq6d_zero_();
+    {
+      const fq6d f0 = s1_get_half<SG>(gf, 0);
+      fq6d_mul_acc1(C, f0, [&](int q) { return s1_get_fq2d<SG>(gf, 3 + q); });
+    }
+    C = fq6d_reduce(fq6d_neg(fq6d_add(C, C)));
+    HBX_SEQ();
+    fq6d T1 = fq6d_zero_();
+    fq6d_mul_acc1(T1, C, [&](int q) { return s1_get_fq2d<S>(a, q); });
+    r.c1 = fq6d_reduce(T1);
+  }
   HBX_SEQ();
-  fq6d A = fq6d_zero_();
-  fq6d_mul_acc1(A, s1_get_half<SG>(gg, 0), [&](int q) { return s1_get_fq2d<S>(a, q); });
-  HBX_SEQ();
-  fq6d B = fq6d_zero_();
-  fq6d_mul_acc1(B, s1_get_half<SG>(gg, 1), [&](int q) { return s1_get_fq2d<S>(a, q); });
-  fq12d r{fq6d_reduce(A), fq6d_reduce(B)};  // t0 = conj(f) / f
+  {
+    // t0.c0 = (A + B) N^-1
+    fq6d T0 = fq6d_zero_();
+    fq6d_mul_acc1(T0, s1_get_half<SG>(gg, 0), [&](int q) { return s1_get_fq2d<S>(a, q); });
+    r.c0 = fq6d_reduce(T0);  // t0 = conj(f) / f
+  }
   HBX_SEQ();
   s1_put_fq12d<S>(a, r);
   HBX_SEQ();

@@ -300,6 +300,46 @@ HBX_HD void fqd_redc2(Col col, fqd& rx, fqd& ry) {
   ry.d[13] = (int32_t)ay;
 }
 
+// N Montgomery reductions driven by one column loop (fqd_redc2 for any N): col(k, jlo, jhi, X)
+// gives column k of each of the N double-width values (X[q] exact in int64); r[q] = x_q / 2^392 mod
+// p, normalised.  A product whose outputs are sums of several digit convolutions reduces each
+// output ONCE (lazy reduction) instead of once per convolution's Fq2 product.
+template <int N, class Col>
+HBX_HD void fqd_redcn(Col col, fqd (&r)[N]) {
+  uint32_t mm[N][14];
+  int64_t acc[N];
+#pragma unroll
+  for (int q = 0; q < N; q++) acc[q] = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int jlo = k < 14 ? 0 : k - 13;
+    const int jhi = k < 14 ? k : 13;
+    int64_t X[N];
+    col(k, jlo, jhi, X);
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+      uint64_t u = 0;
+#pragma unroll
+      for (int j = jlo; j <= jhi; j++)
+        if (j < k - 1) u = (uint64_t)mm[q][j] * FQ_P28[k - j] + u;
+      acc[q] += X[q] + (int64_t)u;
+      if (k >= 1 && k <= 14) acc[q] += (int64_t)((uint64_t)mm[q][k - 1] * FQ_P28[1]);
+      if (k < 14) {
+        mm[q][k] = ((uint32_t)acc[q] * FQ_INV28) & (uint32_t)DMASK;
+        acc[q] += (int64_t)((uint64_t)mm[q][k] * FQ_P28[0]);
+        acc[q] >>= 28;
+      } else {
+        r[q].d[k - 14] = (int32_t)((uint32_t)acc[q] & (uint32_t)DMASK);
+        acc[q] >>= 28;
+        HBX_LAUNDER(r[q].d[k - 14]);
+      }
+    }
+    HBX_COL_FENCE();
+  }
+#pragma unroll
+  for (int q = 0; q < N; q++) r[q].d[13] = (int32_t)acc[q];
+}
+
 // ----------------------------------------------------------------------------------------------
 // Fq2
 // ----------------------------------------------------------------------------------------------
@@ -365,6 +405,50 @@ HBX_HD fq2d fq2d_sqr(const fq2d& a) {
       },
       r.c0, r.c1);
   return r;
+}
+// (a + b Y)^2 in Fq4 = Fq2[Y]/(Y^2 - xi): c0 = a^2 + xi b^2, c1 = 2 a b (the Fq4 squaring of the
+// Granger-Scott and Karabina cyclotomic squarings).  ONE column loop of six digit convolutions --
+// a^2, b^2 and e^2 = (a + b)^2 each as (x0 + x1)(x0 - x1) and x0 x1 -- combined per column into
+// the four output coordinates (c1 = e^2 - a^2 - b^2) and four Montgomery reductions: 6 + 4
+// reductions' worth of multiply-adds instead of three Fq2 squarings' 6 + 6.  a, b normalised;
+// every convolution column is below 14 x 2^57, an output's true column below 2^62.4 (the
+// combination is exact modulo 2^64, so only the true value must fit).  Normalised outputs.
+HBX_HD void fq4d_sqr_lazy(const fq2d& a, const fq2d& b, fq2d& c0, fq2d& c1) {
+  HBX_DBOUND(a.c0, DN); HBX_DBOUND(a.c1, DN); HBX_DBOUND(b.c0, DN); HBX_DBOUND(b.c1, DN);
+  HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL(); HBX_COUNT_FQMUL();
+  const fq2d e = fq2d_norm(fq2d_add(a, b));
+  int32_t sa[14], da[14], sb[14], db[14], se[14], de[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    sa[i] = a.c0.d[i] + a.c1.d[i];
+    da[i] = a.c0.d[i] - a.c1.d[i];
+    sb[i] = b.c0.d[i] + b.c1.d[i];
+    db[i] = b.c0.d[i] - b.c1.d[i];
+    se[i] = e.c0.d[i] + e.c1.d[i];
+    de[i] = e.c0.d[i] - e.c1.d[i];
+  }
+  fqd r[4];
+  fqd_redcn<4>(
+      [&](int k, int jlo, int jhi, int64_t (&X)[4]) {
+        int64_t ar = 0, ai = 0, br = 0, bi = 0, er = 0, ei = 0;
+#pragma unroll
+        for (int j = jlo; j <= jhi; j++) {
+          ar += (int64_t)sa[j] * (int64_t)da[k - j];
+          ai += (int64_t)a.c0.d[j] * (int64_t)a.c1.d[k - j];
+          br += (int64_t)sb[j] * (int64_t)db[k - j];
+          bi += (int64_t)b.c0.d[j] * (int64_t)b.c1.d[k - j];
+          er += (int64_t)se[j] * (int64_t)de[k - j];
+          ei += (int64_t)e.c0.d[j] * (int64_t)e.c1.d[k - j];
+        }
+        // a^2 = (ar, 2 ai), b^2 = (br, 2 bi), e^2 = (er, 2 ei); xi (x + y u) = (x - y) + (x + y) u
+        X[0] = ar + br - 2 * bi;
+        X[1] = 2 * ai + br + 2 * bi;
+        X[2] = er - ar - br;
+        X[3] = 2 * (ei - ai - bi);
+      },
+      r);
+  c0 = fq2d{r[0], r[1]};
+  c1 = fq2d{r[2], r[3]};
 }
 // a * s, s in Fq (two products sharing s)
 HBX_HD fq2d fq2d_mul_fq(const fq2d& a, const fqd& s) {
@@ -450,6 +534,17 @@ HBX_HD fq12d fq12d_mul_by_014(const fq12d& f, const fq2d& c0, const fq2d& c1, co
   const fq2d o = fq2d{fqd_add(c1.c0, c4), c1.c1};
   const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, fq2d_norm(o));
   return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bb), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bb))};
+}
+
+// f * (c0 + c1 v + v w): fq12d_mul_by_014 with c4 = 1 -- a line divided by y_P (an Fq factor the
+// final exponentiation maps to 1).  The c4 product becomes f.c1 v, a coefficient shift: 10 Fq2
+// products instead of 10 plus three Fq-by-Fq2 products.
+HBX_HD fq12d fq12d_mul_by_01v(const fq12d& f, const fq2d& c0, const fq2d& c1) {
+  const fq6d aa = fq6d_mul_by_01(f.c0, c0, c1);
+  const fq2d o = fq2d_norm(fq2d{fqd_add(c1.c0, fqd_const(FQD_ONE)), c1.c1});
+  const fq6d s = fq6d_mul_by_01(fq6d_norm(fq6d_add(f.c1, f.c0)), c0, o);
+  const fq6d bv = fq6d_mul_v(f.c1);  // f.c1 v
+  return fq12d{fq6d_reduce(fq6d_add(fq6d_mul_v(bv), aa)), fq6d_reduce(fq6d_sub(fq6d_sub(s, aa), bv))};
 }
 
 // Granger-Scott cyclotomic squaring (field.hpp fq12_cyclotomic_sqr_t)

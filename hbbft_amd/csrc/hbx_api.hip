@@ -1171,6 +1171,9 @@ int hbx_merkle_proofs(hbx_ctx* c, const uint8_t* nodes, uint32_t inst, uint32_t 
   HBX_STAGE(dr, 5, (size_t)count * 32, "hbx_merkle_proofs");
   HBX_H2D(dn, nodes, nb);
   HBX_H2D(dq, req, (size_t)count * 8);
+  // levels below a proof's depth are not written: zeros, as in a freshly allocated output
+  HIPCHK(c, hipMemsetAsync(dh, 0, (size_t)count * 17 * 32, c->stream));
+  HIPCHK(c, hipMemsetAsync(dsib, 0, (size_t)count * 16 * 32, c->stream));
   int rc = hbx_merkle_proofs_d(c, dn, n, (const uint32_t*)dq, count, dh, dsib, (uint32_t*)dsd,
                                (uint32_t*)dsd + count, dr, c->stream);
   if (rc) return rc;
@@ -1236,6 +1239,7 @@ static int broadcast_decode_host(hbx_ctx* c, uint8_t* shards, const uint8_t* pre
   HBX_H2D(d, shards, all);
   HBX_H2D(dp, present, n * inst);
   HBX_H2D(dre, root_expect, (size_t)inst * 32);
+  HIPCHK(c, hipMemsetAsync(dout, 0, (size_t)inst * out_stride, c->stream));  // bytes past a payload: 0
   int rc = broadcast_decode(c, d, dp, dl, dre, inst, k, m, L, dout, out_stride, (uint64_t*)dlen,
                             (int32_t*)(dlen + (size_t)inst * 8), c->stream);
   if (rc) return rc;

@@ -56,6 +56,10 @@ __device__ __forceinline__ uint8_t share_precheck(int32_t dec_status, bool prese
   return HBX_SHARE_VALID;
 }
 
+#ifndef HBX_ML_SCALED
+#define HBX_ML_SCALED 1  // the one-lane Miller kernel over lines divided by y_P (pairingd.hpp)
+#endif
+
 // Internal status of a share whose pairing check waits for its final exponentiation
 // (k_verify_shares_ml -> k_fe1<6>); never visible outside a verification call.
 constexpr uint8_t SHARE_PENDING = 0xFE;
@@ -506,11 +510,17 @@ __global__ void __launch_bounds__(64) k_verify_shares_ml(const g1a* __restrict__
     const bool skipB = pki.inf || G2pts[2 * j + 1].inf;
     if (!(skipA && skipB)) {
       lds_u32* slot = (lds_u32*)(park + threadIdx.x);
+#if HBX_ML_SCALED
+      // lines divided by y_P (pairingd.hpp miller_loop2_scaled_d): (x/y, 1/y) of S and of -[m] pk_i
+      park_scaled_points(slot, sh.x, sh.y, sh.inf, pki.x, fq_neg(pki.y), pki.inf);
+      const fq12d fd = miller_loop2_scaled_d(lines[j].h, !skipA, lines[j].w, !skipB, slot);
+#else
       park_put_fqd(slot, 0, fqd_from_fq(sh.x));
       park_put_fqd(slot, 1, fqd_from_fq(sh.y));
       park_put_fqd(slot, 2, fqd_from_fq(pki.x));
       park_put_fqd(slot, 3, fqd_neg(fqd_from_fq(pki.y)));
       const fq12d fd = miller_loop2_parked_d(lines[j].h, !skipA, lines[j].w, !skipB, slot);
+#endif
       uint32_t* gf = gslot + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (3 * FE1_WORDS * 64) + threadIdx.x;
       s1_put_fq12d<64>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
       res = SHARE_PENDING;

@@ -220,6 +220,47 @@ HBX_HD fq12d miller_loop2_parked_d(const line_pre_d* LA, bool useA, const line_p
   return fq12d_conj(f);
 }
 
+// miller_loop2_parked_d over lines divided by y_P: the slot holds (x_A / y_A, 1 / y_A,
+// x_B / y_B, 1 / y_B) (park_scaled_points), each line becomes (c0 / y) + (c1 x / y) v + v w and its
+// product costs two Fq-by-Fq2 products for the scaled coefficients instead of one plus the three
+// of the c4 = y term (fq12d_mul_by_01v).  The element differs from miller_loop2_parked_d's by a
+// product of Fq factors (1 / y per line), which the final exponentiation maps to 1: the same verdict.
+HBX_HD fq12d miller_loop2_scaled_d(const line_pre_d* LA, bool useA, const line_pre_d* LB, bool useB,
+                                   const lds_u32* park) {
+  fq12d f = fq12d_one();
+  int k = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fq12d_sqr(f);
+    const int steps = ((BLS_X >> i) & 1) ? 4 : 2;  // (A, B) lines of the doubling [+ addition]
+#pragma unroll 1
+    for (int s = 0; s < steps; s++) {
+      const bool b = (s & 1) != 0;
+      const line_pre_d L = ld_uniform((b ? LB : LA) + k);
+      if (b ? useB : useA) {
+        HBX_SEQ();
+        const fqd w = park_get_fqd(park, b ? 2 : 0);
+        const fqd u = park_get_fqd(park, b ? 3 : 1);
+        f = fq12d_mul_by_01v(f, fq2d_mul_fq(L.c0, u), fq2d_mul_fq(L.c1, w));
+      }
+      if (b) k++;
+    }
+  }
+  return fq12d_conj(f);
+}
+// (x / y, 1 / y) of the two affine G1 points into the slot (words 0..3), one Fq inversion for both
+// (Montgomery's trick); a point at infinity contributes 1 (its pair is not used)
+HBX_HD void park_scaled_points(lds_u32* park, const fq& ax, const fq& ay, bool ainf, const fq& bx, const fq& by,
+                               bool binf) {
+  const fq ya = ainf ? fq_one() : ay, yb = binf ? fq_one() : by;
+  const fq inv = fq_inv_i(fq_mul(ya, yb));
+  const fq ua = fq_mul(inv, yb), ub = fq_mul(inv, ya);
+  park_put_fqd(park, 0, fqd_from_fq(fq_mul(ax, ua)));
+  park_put_fqd(park, 1, fqd_from_fq(ua));
+  park_put_fqd(park, 2, fqd_from_fq(fq_mul(bx, ub)));
+  park_put_fqd(park, 3, fqd_from_fq(ub));
+}
+
 // miller_loop_gen_d with (qx, qy, bx, by) parked in this lane's LDS slot (free until the final
 // exponentiation): 84 registers fewer across the loop; the add steps and every line evaluation
 // read them back.  Same element, same T.  (Parking T as well, Q re-read from memory at the add

@@ -146,6 +146,30 @@ def test_digit_tower_products(hc):
             assert int.from_bytes(out.raw[48:], "big") == (a0 * b1 + a1 * b0) % P
 
 
+def test_fq4d_sqr_lazy(hc):
+    """fieldd.hpp fq4d_sqr_lazy ((a + b Y)^2, Y^2 = xi, six convolutions and four reductions in one
+    column loop: the Karabina and Granger-Scott squarings of the final exponentiation) equals the
+    Fq4 square, with inputs at both ends of the normalised range (x - p, x + p; HBX_DCHECK on)."""
+    rnd = random.Random(24)
+    P = bls.P
+    vals = [0, 1, P - 1, P - 2, (P - 1) // 2] + [rnd.randrange(P) for _ in range(60)]
+    for trial in range(200):
+        x = [rnd.choice(vals) for _ in range(4)]
+        sh = [rnd.choice((-1, 0, 1)) if x[q] else rnd.choice((0, 1)) for q in range(4)]
+        if trial < 16:  # every input at its largest
+            x, sh = [P - 1] * 4, [1] * 4
+        out = ctypes.create_string_buffer(192)
+        hc.hc_fq4d_sqr_lazy(b"".join(_be(v) for v in x), (ctypes.c_int * 4)(*sh), out)
+        a0, a1, b0, b1 = x
+        # a^2 + xi b^2 and 2ab over Fq2 = Fq[u]/(u^2 + 1), xi = 1 + u
+        a2 = ((a0 * a0 - a1 * a1), 2 * a0 * a1)
+        b2 = ((b0 * b0 - b1 * b1), 2 * b0 * b1)
+        want = [(a2[0] + b2[0] - b2[1]) % P, (a2[1] + b2[0] + b2[1]) % P,
+                2 * (a0 * b0 - a1 * b1) % P, 2 * (a0 * b1 + a1 * b0) % P]
+        got = [int.from_bytes(out.raw[48 * q:48 * q + 48], "big") for q in range(4)]
+        assert got == want, (trial, x, sh)
+
+
 def test_digit_tower_pairing_check(hc):
     """The share check's digit-form Miller loop and final exponentiation (pairingd.hpp, the code
     of k_verify_shares) give the same Fq12 elements as pairing.hpp's on the same prepared lines,

@@ -128,7 +128,15 @@ int hc_miller2_digit_cmp(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb
   const fq* y = &e2.c0.c0.c0;
   int same_fe = 1;
   for (int i = 0; i < 12; i++) same_fe &= fq_eq(x[i], y[i]) ? 1 : 0;
-  return same + 2 * same_fe;
+  // the loop over lines divided by y_P (miller_loop2_scaled_d, the one-lane Miller kernel): a
+  // different element (Fq factors), the same element after the final exponentiation
+  park_scaled_points(park, PA.x, PA.y, false, PB.x, PB.y, false);
+  const fq12 gs = fq12d_to_fq12(miller_loop2_scaled_d(DA, true, DB, true, park));
+  const fq12 e3 = final_exponentiation(gs);
+  const fq* z = &e3.c0.c0.c0;
+  int same_scaled = 1;
+  for (int i = 0; i < 12; i++) same_scaled &= fq_eq(x[i], z[i]) ? 1 : 0;
+  return same + 2 * same_fe * same_scaled;
 }
 // The final exponentiation as k_fe1's five steps (fe1d.hpp) on host slots, against
 // final_exponentiation_d on the same Miller output: 1 = the same element, + 2 if the verdicts
@@ -206,6 +214,21 @@ void hc_fq2d_mul(const uint8_t* a, const uint8_t* b, uint8_t* out, int sqr) {
   const fq2d r = sqr ? fq2d_sqr(x) : fq2d_mul(x, y);
   fq_to_be(fq_from_mont(fqd_to_fq(r.c0)), out);
   fq_to_be(fq_from_mont(fqd_to_fq(r.c1)), out + 48);
+}
+// fq4d_sqr_lazy on (a, b) = 4 canonical Fq (BE) each shifted by shift[q] p (-1, 0, 1: the ends of the
+// normalised range), against the product itself: out = canonical c0 || c1 (4 x 48 BE)
+void hc_fq4d_sqr_lazy(const uint8_t* in, const int* shift, uint8_t* out) {
+  fqd v[4];
+  for (int q = 0; q < 4; q++) {
+    v[q] = fqd_from_fq(fq_to_mont(fq_from_be(in + 48 * q)));
+    fqd pd;
+    for (int i = 0; i < 14; i++) pd.d[i] = (int32_t)FQ_P28[i] * shift[q];
+    v[q] = fqd_norm(fqd_add(v[q], pd));
+  }
+  fq2d c0, c1;
+  fq4d_sqr_lazy(fq2d{v[0], v[1]}, fq2d{v[2], v[3]}, c0, c1);
+  const fqd* r[4] = {&c0.c0, &c0.c1, &c1.c0, &c1.c1};
+  for (int q = 0; q < 4; q++) fq_to_be(fq_from_mont(fqd_to_fq(*r[q])), out + 48 * q);
 }
 // e(PA, QA) e(PB, QB) == 1 with QA prepared and QB's lines generated on the fly
 int hc_pairing_check_mixed(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, const uint8_t* qb) {
