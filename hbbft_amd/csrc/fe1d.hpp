@@ -24,8 +24,8 @@
 //       t = frob2(t0) t0                                                      -> slot G
 //   F1  a = conj(t^|x| t); t^3 is the value after the first run of t^|x|      -> slot G, T
 //   F2  a = conj(a^|x| a)                                                      -> slot G
-//   F3  b = conj(a^|x|) frob(a)                                                -> slot F
-//   F4  d = t^3 conj(b) frob2(b)                                               -> slot T
+//   F3  b = conj(a^|x|) frob(a) -> slot F, then (same kernel, b from registers)
+//       d = t^3 conj(b) frob2(b)                                               -> slot T
 //   F5  u = b^|x|                                                              -> slot G
 //   F6  u^|x| d == 1  (= b^(x^2) d = f^(3 (p^12 - 1)/r))
 #pragma once
@@ -547,9 +547,10 @@ HBX_HD void fe1_step_expmul(P a, PG gt, PG gg, bool& degenerate) {
   r = fq12d_mul_slot<S>(r, a);
   s1_put_fq12d<SG>(gg, fq12d{r.c0, fq6d_norm(fq6d_neg(r.c1))});
 }
-// F3: b = conj(a^|x|) frob(a)  -> F
+// F3 + F4 in one kernel: b = conj(a^|x|) frob(a) -> F, then d = t^3 conj(b) frob2(b) -> T with b
+// still in registers and put into slot a directly (no reload of F, no kernel boundary)
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step3(P a, PG gf, PG gg, bool& degenerate) {
+HBX_HD void fe1_step34(P a, PG gf, PG gt, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gg);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
@@ -557,17 +558,14 @@ HBX_HD void fe1_step3(P a, PG gf, PG gg, bool& degenerate) {
   HBX_SEQ();
   s1_frob_inplace<S, 1>(a);
   HBX_SEQ();
-  r = fq12d_mul_slot<S>(fq12d_conj(r), a);
+  r = fq12d_mul_slot<S>(fq12d_conj(r), a);  // b
   s1_put_fq12d<SG>(gf, r);
-}
-// F4: d = t^3 conj(b) frob2(b)  -> T
-template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step4(P a, PG gf, PG gt) {
-  s1_copy<S, SG>(a, gf);
+  HBX_SEQ();
+  s1_put_fq12d<S>(a, r);
   HBX_SEQ();
   s1_frob_inplace<S, 2>(a);
   HBX_SEQ();
-  fq12d r = fq12d_mul_slot<S>(fq12d_conj(s1_get_fq12d<SG>(gf)), a);
+  r = fq12d_mul_slot<S>(fq12d_conj(r), a);
   HBX_SEQ();
   s1_copy<S, SG>(a, gt);
   HBX_SEQ();
@@ -601,8 +599,7 @@ HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg, bool& degenerate) {
   fe1_step0<S, SG>(a, gf, gg);
   fe1_step_expmul<S, SG>(a, gt, gg, degenerate);
   fe1_step_expmul<S, SG>(a, (PG) nullptr, gg, degenerate);
-  fe1_step3<S, SG>(a, gf, gg, degenerate);
-  fe1_step4<S, SG>(a, gf, gt);
+  fe1_step34<S, SG>(a, gf, gt, gg, degenerate);
   fe1_step5<S, SG>(a, gf, gg, degenerate);
   return fe1_step6<S, SG>(a, gt, gg, degenerate);
 }

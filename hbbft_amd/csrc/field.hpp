@@ -465,11 +465,15 @@ HBX_HDNI fq fq_pow_const(const fq& a, const uint32_t* e) {
 //   g even:               (delta, f, g) <- (1 + delta, f, g / 2)
 // and depends only on delta and the parity of g, so 30 steps run on the low words of f and g and
 // give an integer matrix T with 2^30 (f', g') = T (f, g) (|entries| <= 2^30); T then updates the
-// full f, g (exact shift) and d, e (mod m, made divisible by 2^30 with a multiple of m).  After
-// floor((49 b + 57) / 17) divsteps (b = 32N bits, Bernstein-Yang's bound) g = 0, f = +-1 and
-// x^-1 = +-d.  Fixed step count and selects only: every lane of a wave runs the same
-// instructions (~30k VALU ops for N = 12, against ~150k for the bit-by-bit binary Euclid this
-// replaced, whose data-dependent branch split the wave).  x = 0 gives 0.
+// full f, g (exact shift) and d, e (mod m, made divisible by 2^30 with a multiple of m).
+// Half-delta variant ("hddivsteps"): delta starts at 1/2 (the steps hold `delta` = 2 delta: start
+// 1, updates 2 - delta / 2 + delta), which lowers the step bound from Bernstein-Yang's
+// floor((49 b + 57) / 17) to floor((45907 b + 26313) / 19929) (b = 32N bits; the bound libsecp256k1's
+// safegcd uses, 590 steps at 256 bits): 886 steps at 381 bits, run as 31 batches of 30 with a
+// margin of one batch (Bernstein-Yang's bound: 37).  After them g = 0, f = +-1 and x^-1 = +-d.
+// Fixed step count and selects only: every lane of a wave runs the same instructions (~30k VALU
+// ops for N = 12, against ~150k for the bit-by-bit binary Euclid this replaced, whose
+// data-dependent branch split the wave).  x = 0 gives 0.
 HBX_HD void divsteps30(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32_t& v, int32_t& q, int32_t& r) {
   int32_t uu = 1, vv = 0, qq = 0, rr = 1;
 #pragma unroll 6
@@ -481,7 +485,7 @@ HBX_HD void divsteps30(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32
     const int32_t nu = sw ? qq : uu, nv = sw ? rr : vv;
     const int32_t nq = sw ? qq - uu : (godd ? qq + uu : qq);
     const int32_t nr = sw ? rr - vv : (godd ? rr + vv : rr);
-    delta = sw ? 1 - delta : 1 + delta;
+    delta = sw ? 2 - delta : 2 + delta;  // 2 delta (half-delta steps)
     f = nf;
     g = ng >> 1;
     uu = nu * 2;
@@ -546,7 +550,7 @@ HBX_HD void lincomb_mod_shr30(const uint32_t* d, const uint32_t* e, int32_t ca, 
 template <int N>
 HBX_HD void binv_limbs(const uint32_t* x, const uint32_t* m, uint32_t* out) {
   constexpr int L = N + 1;
-  constexpr int BATCHES = ((49 * 32 * N + 57) / 17 + 29) / 30;
+  constexpr int BATCHES = ((45907 * 32 * N + 26313) / 19929 + 30 + 29) / 30;  // hddivsteps bound + one batch
   uint32_t f[L], g[L], d[L], e[L];
 #pragma unroll
   for (int i = 0; i < L; i++) {
@@ -558,7 +562,7 @@ HBX_HD void binv_limbs(const uint32_t* x, const uint32_t* m, uint32_t* out) {
   uint32_t minv = m[0];  // Newton: 3 -> 6 -> 12 -> 24 -> 48 correct low bits
 #pragma unroll
   for (int i = 0; i < 4; i++) minv *= 2u - m[0] * minv;
-  int32_t delta = 1;
+  int32_t delta = 1;  // 2 delta, delta = 1/2
 #pragma unroll 1
   for (int b = 0; b < BATCHES; b++) {
     int32_t u, v, q, r;

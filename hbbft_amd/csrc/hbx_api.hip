@@ -844,8 +844,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
       hipLaunchKernelGGL(k_fe1<0>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
       hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
       hipLaunchKernelGGL(k_fe1<2>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
-      hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
-      hipLaunchKernelGGL(k_fe1<4>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);  // F3 + F4
       hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
       hipLaunchKernelGGL(k_fe1<6>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
       // lanes whose compressed squarings met g3 = 0 (never expected): the single-kernel check

@@ -601,10 +601,8 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
     fe1_step_expmul<64, 64>(a, gt, gg, degenerate);
   } else if (STEP == 2) {
     fe1_step_expmul<64, 64>(a, (uint32_t*)nullptr, gg, degenerate);
-  } else if (STEP == 3) {
-    fe1_step3<64, 64>(a, gf, gg, degenerate);
-  } else if (STEP == 4) {
-    fe1_step4<64, 64>(a, gf, gt);
+  } else if (STEP == 3) {  // F3 and F4 in one kernel (fe1d.hpp fe1_step34); there is no k_fe1<4>
+    fe1_step34<64, 64>(a, gf, gt, gg, degenerate);
   } else if (STEP == 5) {
     fe1_step5<64, 64>(a, gf, gg, degenerate);
   } else {
@@ -619,7 +617,6 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
 // the steps compile in three translation units (tools/build.py): each is a large kernel
 #if HBX_IN_TU(8)
 template __global__ void k_fe1<0>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
-template __global__ void k_fe1<4>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 template __global__ void k_fe1<6>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #elif HBX_IN_TU(9)
 template __global__ void k_fe1<1>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);

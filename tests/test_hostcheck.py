@@ -301,6 +301,45 @@ def test_heff_scaled_hash_point(hc):
     assert out.raw == bls.g1_compress(bls.g1_mul(pk, m))
 
 
+def _slow_gcd_inputs(mod):
+    """Inputs with long continued fractions against the modulus (x / m near 1/phi, and neighbours):
+    the slowest gcds."""
+    a, b = 1, 1
+    while b < mod << 8:  # consecutive Fibonacci numbers: b / a -> phi to 2 x 392 bits
+        a, b = b, a + b
+    out = []
+    for k in range(-40, 41):
+        x = mod * a // b + k
+        out += [x % mod, (mod - x) % mod, (2 * x) % mod]
+    return [x for x in out if x]
+
+
+def _hddivsteps_needed(x, m):
+    """Steps the half-delta divstep recurrence (field.hpp binv_limbs) takes until g = 0."""
+    delta, f, g, n = 1, m, x, 0  # 2 delta
+    while g:
+        if delta > 0 and g & 1:
+            delta, f, g = 2 - delta, g, (g - f) // 2
+        elif g & 1:
+            delta, g = 2 + delta, (g + f) // 2
+        else:
+            delta, g = 2 + delta, g // 2
+        n += 1
+    return n
+
+
+def test_hddivsteps_bound():
+    """binv_limbs runs 31 batches of 30 half-delta divsteps at 381 bits (21 at 255 bits): the
+    recurrence reaches g = 0 well inside that on random and slow-gcd inputs; the bound it relies on
+    (floor((45907 b + 26313) / 19929), libsecp256k1's safegcd) is 886 / 590 steps."""
+    rnd = random.Random(31)
+    for mod, bits, batches in ((bls.P, 384, 31), (bls.R, 256, 21)):
+        bound = (45907 * bits + 26313) // 19929
+        assert bound <= 30 * batches - 30
+        worst = max(_hddivsteps_needed(x, mod) for x in _slow_gcd_inputs(mod) + [rnd.randrange(1, mod) for _ in range(3000)])
+        assert worst <= bound, (mod, worst, bound)
+
+
 def test_binv_divsteps(hc):
     """binv_limbs (batched Bernstein-Yang divsteps, every inversion of the kernels) against
     Python's modular inverse, mod p and mod r, on random and edge values (0 -> 0)."""
@@ -309,6 +348,8 @@ def test_binv_divsteps(hc):
         vals = [0, 1, 2, 3, mod - 1, mod - 2, (mod + 1) // 2, 1 << 31, (1 << (32 * nl - 4)) % mod]
         vals += [rnd.randrange(mod) for _ in range(300)]
         vals += [rnd.randrange(1 << rnd.randrange(1, 40)) for _ in range(50)]  # short values
+        vals += _slow_gcd_inputs(mod)
+        vals += [rnd.randrange(mod) for _ in range(3000)]
         for x in vals:
             xa = (ctypes.c_uint32 * nl)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(nl)])
             out = (ctypes.c_uint32 * nl)()

@@ -197,8 +197,7 @@ int hc_fe1_step0_one(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, co
   bool degenerate = false;
   fe1_step_expmul<1, 1>(a, gt, gg, degenerate);
   fe1_step_expmul<1, 1>(a, (uint32_t*)nullptr, gg, degenerate);
-  fe1_step3<1, 1>(a, gf, gg, degenerate);
-  fe1_step4<1, 1>(a, gf, gt);
+  fe1_step34<1, 1>(a, gf, gt, gg, degenerate);
   fe1_step5<1, 1>(a, gf, gg, degenerate);
   const bool v = fq12d_is_one_seq(fe1_step6<1, 1>(a, gt, gg, degenerate));
   return (one ? 1 : 0) + (degenerate ? 2 : 0) + (v ? 4 : 0);
