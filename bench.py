@@ -1259,7 +1259,7 @@ def main():
     kern = eb.kernel_ms()
     ctx.set_timing(False)
     lanes = ctx.verify_lanes_used()
-    kname = {1: "k_verify_shares_ml + k_fe1<0,1,2,3,5,6> (+ k_verify_shares for fallback lanes; one timed region)",
+    kname = {1: "k_verify_shares_ml + k_fe1<0,1,3,5> (+ k_verify_shares for fallback lanes; one timed region)",
              2: "k_verify_shares2", 3: "k_verify_shares3", 6: "k_verify_shares6",
              7: "k_verify_shares (single kernel)"}.get(lanes, "k_verify_shares")
     traffic = traffic_record() if (n == 256 and pj == 256) else None

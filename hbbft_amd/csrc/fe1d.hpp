@@ -19,7 +19,9 @@
 // Every step is one kernel, so the register allocator sees at most one exponentiation loop and
 // two products at a time, and there are no call frames at all.
 //
-// Chain (pairing.hpp final_exponentiation, regrouped as pairing2d.hpp FE2_PROG), one kernel each:
+// Chain (pairing.hpp final_exponentiation, regrouped as pairing2d.hpp FE2_PROG), four kernels
+// (F0, F1 + F2, F3 + F4, F5 + F6; a pair shares one kernel: its hand-over stays in registers and
+// LDS):
 //   F0  t0 = conj(f)^2 / N(f) (= conj(f) f^-1, N(f) = f0^2 - v f1^2 in Fq6: one Fq6 inverse);
 //       t = frob2(t0) t0                                                      -> slot G
 //   F1  a = conj(t^|x| t); t^3 is the value after the first run of t^|x|      -> slot G, T
@@ -452,7 +454,8 @@ HBX_HD bool fq12d_is_one_seq(const fq12d& a) {
 
 // ---- the seven steps over a lane's slots: a = LDS (or host) slot, gf / gt / gg = global slots F
 // (Miller output, later b), T (t^3, later d), G (t, a, u) ------------------------------------------
-constexpr int FE1_STEPS = 7;
+constexpr int FE1_STEPS = 7;  // F0..F6; run as four kernels: k_fe1<0>, <1> (F1 + F2), <3> (F3 + F4), <5> (F5 + F6)
+constexpr int FE1_LAST = 5;   // the kernel that decides the verdict
 // F0: t = frob2(t0) t0, t0 = conj(f) / f  -> G
 template <int SG, class PG>
 HBX_HD fq6d s1_get_half(PG p, int h) {
@@ -536,16 +539,25 @@ HBX_HD bool fe1_step0(P a, PG gf, PG gg) {
   // in Fq6 and t = 1 (tests/test_gpu_threshold.py::test_degenerate_ciphertext_r_m).
   return fq12d_is_one_seq(r);
 }
-// F1, F2: x -> conj(x^|x| x) (x = t: t^3 -> T on the way; then x = a)
+// F1 + F2 in one kernel: x -> conj(x^|x| x) twice (x = t, t^3 -> T on the way; then x = a), the
+// intermediate a handed over in registers and slot a (no store / reload through G, no kernel
+// boundary); the loop keeps one copy of the code
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step_expmul(P a, PG gt, PG gg, bool& degenerate) {
+HBX_HD void fe1_step12(P a, PG gt, PG gg, bool& degenerate) {
   s1_copy<S, SG>(a, gg);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, gt, degenerate);
-  HBX_SEQ();
-  r = fq12d_mul_slot<S>(r, a);
-  s1_put_fq12d<SG>(gg, fq12d{r.c0, fq6d_norm(fq6d_neg(r.c1))});
+#pragma unroll 1
+  for (int rep = 0; rep < 2; rep++) {
+    r = cyc_exp_abs_x_slot<S, SG>(r, a, rep == 0 ? gt : (PG) nullptr, degenerate);
+    HBX_SEQ();
+    r = fq12d_mul_slot<S>(r, a);
+    r = fq12d{r.c0, fq6d_norm(fq6d_neg(r.c1))};
+    HBX_SEQ();
+    if (rep == 0) s1_put_fq12d<S>(a, r);
+    HBX_SEQ();
+  }
+  s1_put_fq12d<SG>(gg, r);
 }
 // F3 + F4 in one kernel: b = conj(a^|x|) frob(a) -> F, then d = t^3 conj(b) frob2(b) -> T with b
 // still in registers and put into slot a directly (no reload of F, no kernel boundary)
@@ -572,23 +584,20 @@ HBX_HD void fe1_step34(P a, PG gf, PG gt, PG gg, bool& degenerate) {
   r = fq12d_mul_slot<S>(r, a);
   s1_put_fq12d<SG>(gt, r);
 }
-// F5: u = b^|x|  -> G
+// F5 + F6 in one kernel: u = b^|x|, then u^|x| d (= b^(x^2) d = f^(3 (p^12 - 1)/r)), == 1 iff the
+// check holds; u handed over in registers and slot a
 template <int S, int SG, class P, class PG>
-HBX_HD void fe1_step5(P a, PG gf, PG gg, bool& degenerate) {
+HBX_HD fq12d fe1_step56(P a, PG gf, PG gt, bool& degenerate) {
   s1_copy<S, SG>(a, gf);
   HBX_SEQ();
   fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
-  s1_put_fq12d<SG>(gg, r);
-}
-// F6: u^|x| d (= b^(x^2) d = f^(3 (p^12 - 1)/r)): == 1 iff the check holds
-template <int S, int SG, class P, class PG>
-HBX_HD fq12d fe1_step6(P a, PG gt, PG gg, bool& degenerate) {
-  s1_copy<S, SG>(a, gg);
-  HBX_SEQ();
-  fq12d r = s1_get_fq12d<S>(a);
-  r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
-  HBX_SEQ();
+#pragma unroll 1
+  for (int rep = 0; rep < 2; rep++) {
+    r = cyc_exp_abs_x_slot<S, SG>(r, a, (PG) nullptr, degenerate);
+    HBX_SEQ();
+    if (rep == 0) s1_put_fq12d<S>(a, r);
+    HBX_SEQ();
+  }
   s1_copy<S, SG>(a, gt);
   HBX_SEQ();
   return fq12d_mul_slot<S>(r, a);
@@ -597,11 +606,9 @@ HBX_HD fq12d fe1_step6(P a, PG gt, PG gg, bool& degenerate) {
 template <int S, int SG, class P, class PG>
 HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg, bool& degenerate) {
   fe1_step0<S, SG>(a, gf, gg);
-  fe1_step_expmul<S, SG>(a, gt, gg, degenerate);
-  fe1_step_expmul<S, SG>(a, (PG) nullptr, gg, degenerate);
+  fe1_step12<S, SG>(a, gt, gg, degenerate);
   fe1_step34<S, SG>(a, gf, gt, gg, degenerate);
-  fe1_step5<S, SG>(a, gf, gg, degenerate);
-  return fe1_step6<S, SG>(a, gt, gg, degenerate);
+  return fe1_step56<S, SG>(a, gf, gt, degenerate);
 }
 
 }  // namespace hbx

@@ -70,6 +70,7 @@ struct hbx_ctx {
   uint32_t n_keys = 0;
   dbuf comb_partial, comb_done;  // k_combine_q: per-block partial sums, per-proposer block counters
   dbuf pk, pk_m, pk64, pk_status, pk_comp;  // pk_m = [3(x^2-1)] pk, pk64 = [2^64] pk (k_scale_keys)
+  dbuf g1tab;  // fixed-base tables of the key shares, [n][64][15] affine (k_g1_tables; coin master identity)
   // epoch state
   uint32_t p_ct = 0;
   dbuf U, G2pts, Hj, lines, lines_d, scratch, ct_ok, ct_valid, dec_st;
@@ -480,7 +481,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
   timing_reset(c);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->ev_pool.clear();
-  dbuf* bufs[] = {&c->comb_partial, &c->comb_done, &c->pk,       &c->pk_m,       &c->pk64,       &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
+  dbuf* bufs[] = {&c->comb_partial, &c->comb_done, &c->pk,       &c->pk_m,       &c->pk64,       &c->g1tab,      &c->pk_status,  &c->pk_comp,     &c->U,         &c->G2pts, &c->Hj,
                   &c->lines,    &c->scratch,    &c->ct_ok,       &c->ct_valid,  &c->v_blob_own,
                   &c->v_off_own, &c->u_comp_own, &c->w_comp_own, &c->S,         &c->valid,
                   &c->S_status, &c->fallback, &c->gslot,
@@ -581,6 +582,14 @@ int hbx_set_pk_shares(hbx_ctx* c, const uint8_t* pk_comp, uint32_t n, int32_t* s
     hipLaunchKernelGGL(k_scale_keys, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->pk.as<g1a>(), n,
                        c->pk_m.as<g1a>(), c->pk64.as<g1a>());
     HIPCHK(c, hipGetLastError());
+    // [d 16^w] pk_i for the coin combine's master identity (k_combine_sigs): era set-up, not per round
+    if (!c->g1tab.ensure((size_t)n * G1TAB_W * G1TAB_D * sizeof(g1a)))
+      return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_set_pk_shares: out of device memory (key tables)");
+    hipLaunchKernelGGL(k_g1_tables, dim3((n * G1TAB_W + 63) / 64), dim3(64), 0, c->stream, c->pk.as<g1a>(), n,
+                       c->g1tab.as<g1a>());
+    HIPCHK(c, hipGetLastError());
+  } else {
+    c->g1tab.release();  // no tables of an older key set
   }
   std::vector<int32_t> st(n);
   HIPCHK(c, hipMemcpyAsync(st.data(), c->pk_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -842,11 +851,9 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
       const uint8_t* ctok = c->ct_ok.as<uint8_t>();
       uint8_t* vd = c->valid.as<uint8_t>();
       hipLaunchKernelGGL(k_fe1<0>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
-      hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
-      hipLaunchKernelGGL(k_fe1<2>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<1>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);  // F1 + F2
       hipLaunchKernelGGL(k_fe1<3>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);  // F3 + F4
-      hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
-      hipLaunchKernelGGL(k_fe1<6>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);
+      hipLaunchKernelGGL(k_fe1<5>, grid, dim3(64), 0, s, gs, n, vd, ctok, me, ctv, c->force_fallback);  // F5 + F6
       // lanes whose compressed squarings met g3 = 0 (never expected): the single-kernel check
       hipLaunchKernelGGL(k_verify_shares, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(), d_present,
                          c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(), ctok, n, vd,
@@ -1606,7 +1613,8 @@ static int combine_sigs_impl(hbx_ctx* c, const uint8_t* master_pk48, uint32_t t,
     timed t_(c, HBX_K_COMBINE_SIGS, s);
     hipLaunchKernelGGL(k_combine_sigs, dim3(I), dim3(SIGCOMB_THREADS), 0, s, valid, c->coin_sig.as<g2a>(), c->coin_n, t,
                        c->pk.as<g1a>(), c->pk64.as<g1a>(), c->coin_mpk.as<g1a>(), c->coin_comb.as<g2a>(),
-                       c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>());
+                       c->coin_comb_st.as<int32_t>(), c->coin_ok.as<uint8_t>(),
+                       c->g1tab.p ? c->g1tab.as<g1a>() : nullptr);
   }
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_sig_parity, dim3((I + 63) / 64), dim3(64), 0, s, c->coin_comb.as<g2a>(), c->coin_comb_st.as<int32_t>(),

@@ -20,6 +20,7 @@
 #include "pairing3d.hpp"
 #include "pairing2d.hpp"
 #include "fe1d.hpp"
+#include "g2d.hpp"
 #include "curve4.hpp"
 #include "wide.hpp"
 
@@ -97,6 +98,9 @@ __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict_
   status[i] = st;
 }
 #endif
+
+// Fixed-base tables of the key shares (k_g1_tables): 64 windows of 4 bits, digits 1..15.
+constexpr int G1TAB_W = 64, G1TAB_D = 15;
 
 // Lanes per hash_g2 group (hash.hpp hash_g2_group).
 constexpr int HASH_K = 16;
@@ -580,7 +584,7 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   const size_t idx = (size_t)j * n + i;
   const uint8_t st = valid[idx];
   if (st != SHARE_PENDING) {
-    if (STEP == FE1_STEPS - 1 && i == me && ct_valid && st != SHARE_FALLBACK)
+    if (STEP == FE1_LAST && i == me && ct_valid && st != SHARE_FALLBACK)
       ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : st == HBX_SHARE_VALID ? HBX_CT_VALID : HBX_CT_INVALID;
     return;
   }
@@ -597,16 +601,12 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
       if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : HBX_CT_VALID;
       return;
     }
-  } else if (STEP == 1) {
-    fe1_step_expmul<64, 64>(a, gt, gg, degenerate);
-  } else if (STEP == 2) {
-    fe1_step_expmul<64, 64>(a, (uint32_t*)nullptr, gg, degenerate);
-  } else if (STEP == 3) {  // F3 and F4 in one kernel (fe1d.hpp fe1_step34); there is no k_fe1<4>
+  } else if (STEP == 1) {  // F1 + F2
+    fe1_step12<64, 64>(a, gt, gg, degenerate);
+  } else if (STEP == 3) {  // F3 + F4
     fe1_step34<64, 64>(a, gf, gt, gg, degenerate);
-  } else if (STEP == 5) {
-    fe1_step5<64, 64>(a, gf, gg, degenerate);
-  } else {
-    const bool v = fq12d_is_one_seq(fe1_step6<64, 64>(a, gt, gg, degenerate));
+  } else {  // F5 + F6: the verdict
+    const bool v = fq12d_is_one_seq(fe1_step56<64, 64>(a, gf, gt, degenerate));
     if (!degenerate) {
       valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
       if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : v ? HBX_CT_VALID : HBX_CT_INVALID;
@@ -614,16 +614,14 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   }
   if (degenerate) valid[idx] = SHARE_FALLBACK;
 }
-// the steps compile in three translation units (tools/build.py): each is a large kernel
+// the four step kernels compile in three translation units (tools/build.py): each is a large kernel
 #if HBX_IN_TU(8)
 template __global__ void k_fe1<0>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
-template __global__ void k_fe1<6>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
+template __global__ void k_fe1<5>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #elif HBX_IN_TU(9)
 template __global__ void k_fe1<1>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
-template __global__ void k_fe1<2>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #else
 template __global__ void k_fe1<3>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
-template __global__ void k_fe1<5>(uint32_t*, uint32_t, uint8_t*, const uint8_t*, uint32_t, uint8_t*, uint32_t);
 #endif
 #endif
 
@@ -1413,6 +1411,27 @@ __global__ void __launch_bounds__(64) k_scale_keys(const g1a* __restrict__ pk, u
   for (int d = 0; d < 64; d++) q = g1_dbl(q);
   pk64[i] = g1_to_affine(q);
 }
+// Fixed-base tables of the key shares (once per key set, hbx_set_pk_shares): tab[(i * 64 + w) * 15 +
+// d - 1] = [d 16^w] pk_i (affine), d = 1..15, w = 0..63 -- the coin combine's master identity
+// sum_k lambda_k pk_k then costs one mixed addition per nonzero 4-bit digit of lambda_k and no
+// doublings (k_combine_sigs).  One lane per (key, window): 4w doublings, 14 additions.
+__global__ void __launch_bounds__(64) k_g1_tables(const g1a* __restrict__ pk, uint32_t n, g1a* __restrict__ tab) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = gid / G1TAB_W, w = gid % G1TAB_W;
+  if (i >= n) return;
+  g1j b = g1_from_affine(pk[i]);
+#pragma unroll 1
+  for (uint32_t d = 0; d < 4 * w; d++) b = g1_dbl(b);
+  const g1a ba = g1_to_affine(b);
+  g1a* out = tab + ((size_t)i * G1TAB_W + w) * G1TAB_D;
+  out[0] = ba;
+  g1j acc = b;
+#pragma unroll 1
+  for (int d = 2; d <= G1TAB_D; d++) {
+    acc = g1_add_mixed_i(acc, ba);
+    out[d - 1] = g1_to_affine(acc);
+  }
+}
 // H_j = hash_g1_g2(U_j, V_j) itself from H'_j = h_eff P (hbx_get_ct_hashes), compressed.
 __global__ void __launch_bounds__(64) k_true_hashes(const g2a* __restrict__ G2pts, const g2j* __restrict__ Hj,
                                                     uint32_t count, uint8_t* __restrict__ out96) {
@@ -1607,6 +1626,16 @@ __device__ __forceinline__ fq fq_shfl_xor(const fq& a, int m) {
   for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__shfl_xor((int)a.l[i], m);
   return r;
 }
+__device__ __forceinline__ fqd fqd_shfl_xor(const fqd& a, int m) {
+  fqd r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = __shfl_xor(a.d[i], m);
+  return r;
+}
+__device__ __forceinline__ g2jd g2jd_shfl_xor(const g2jd& a, int m) {
+  return g2jd{fq2d{fqd_shfl_xor(a.x.c0, m), fqd_shfl_xor(a.x.c1, m)}, fq2d{fqd_shfl_xor(a.y.c0, m), fqd_shfl_xor(a.y.c1, m)},
+              fq2d{fqd_shfl_xor(a.z.c0, m), fqd_shfl_xor(a.z.c1, m)}};
+}
 __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
   return g2j{fq2{fq_shfl_xor(a.x.c0, m), fq_shfl_xor(a.x.c1, m)}, fq2{fq_shfl_xor(a.y.c0, m), fq_shfl_xor(a.y.c1, m)},
              fq2{fq_shfl_xor(a.z.c0, m), fq_shfl_xor(a.z.c1, m)}};
@@ -1641,7 +1670,8 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
                                                                   const g1a* __restrict__ pk64,
                                                                   const g1a* __restrict__ master_pk,
                                                                   g2a* __restrict__ out, int32_t* __restrict__ status,
-                                                                  uint8_t* __restrict__ master_ok) {
+                                                                  uint8_t* __restrict__ master_ok,
+                                                                  const g1a* __restrict__ g1tab) {
   // One block per instance: waves 0..2 the G2 combine (four psi-digit lanes per share), wave 3 the
   // G1 master identity (two GLV lanes per share).  At t = 43 that is 172 + 86 tasks on 256 threads
   // in ONE round of blocks (a block row per part made 512 one-wave-per-SIMD blocks, two rounds).
@@ -1675,8 +1705,20 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
     __syncthreads();
   }
   g1j acc1 = g1_identity();
-  g2j acc2 = g2_identity();
-  if (g1_part) {
+  if (g1_part && g1tab) {
+    // fixed-base tables (k_g1_tables): lane w sums window w of every term,
+    // sum_k [nibble_w(lambda_k) 16^w] pk_k, one mixed addition per nonzero nibble; the tree below
+    // adds the 64 window sums
+    const int w = tid - G2_THREADS;
+#pragma unroll 1
+    for (int k = 0; k < (int)t; k++) {
+      const fr lam = lds_lam ? lam_s[k] : lagrange_at_zero(idx, (int)t, k);
+      const uint32_t nib = (lam.l[w >> 3] >> ((w & 7) * 4)) & 15u;
+      if (nib) acc1 = g1_add_mixed_i(acc1, g1tab[((size_t)idx[k] * G1TAB_W + w) * G1TAB_D + nib - 1]);
+    }
+#pragma unroll 1
+    for (int m = 1; m < 64; m <<= 1) acc1 = g1_add(acc1, g1j_shfl_xor(acc1, m));
+  } else if (g1_part) {
     // four 64-bit tasks per share: GLV half h of lambda_k = lo + 2^64 hi, [lo] P_h + [hi] [2^64] P_h
     // with P_0 = pk_k, P_1 = phi(pk_k) (4t tasks of 60 doublings on the wave's 64 lanes instead of
     // 2t of 124: the master identity no longer outlasts the G2 sum)
@@ -1694,19 +1736,24 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
 #pragma unroll 1
     for (int m = 1; m < 64; m <<= 1) acc1 = g1_add(acc1, g1j_shfl_xor(acc1, m));
   } else {
+    // the G2 half in the digit tower (g2d.hpp): the 64-bit multiplications and the lane tree
+    g2jd a2 = g2d_identity();
     for (int q = tid; q < 4 * (int)t; q += G2_THREADS) {
       const int k = q >> 2, i = q & 3;
       const fr lam = lds_lam ? lam_s[k] : lagrange_at_zero(idx, (int)t, k);
       uint64_t d[4];
       fr_base_x_digits(lam.l, d);
-      g2j P = g2_from_affine(sig[(size_t)inst * n + idx[k]]);
+      const g2a S = sig[(size_t)inst * n + idx[k]];
+      if (d[i] == 0 || S.inf) continue;
+      g2j P = g2_from_affine(S);
       for (int e = 0; e < i; e++) P = g2_psi(P);  // affine in, affine out (Z = 1)
-      g2a Pa{P.x, i & 1 ? fq2_neg(P.y) : P.y, false};
-      if (d[i] != 0) acc2 = g2_add(acc2, g2_mul_u64_w4(Pa, d[i]));
+      bool rinf;
+      const g2jd R = g2d_mul_u64_w4(fq2d_from_fq2(P.x), fq2d_from_fq2(i & 1 ? fq2_neg(P.y) : P.y), d[i], rinf);
+      if (!rinf) a2 = g2d_add(a2, R);
     }
 #pragma unroll 1
-    for (int m = 1; m < 64; m <<= 1) acc2 = g2_add(acc2, g2j_shfl_xor(acc2, m));
-    if ((tid & 63) == 0) red2[tid >> 6] = acc2;
+    for (int m = 1; m < 64; m <<= 1) a2 = g2d_add(a2, g2jd_shfl_xor(a2, m));
+    if ((tid & 63) == 0) red2[tid >> 6] = g2jd_to_g2j(a2);
   }
   __syncthreads();
   if (tid == 0) {

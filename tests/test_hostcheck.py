@@ -487,12 +487,26 @@ def test_g2_membership_from_miller_T(hc):
 
 
 def test_g2_mul_u64_windows_match_naf(hc):
-    """k_combine_sigs' 64-bit G2 multiplications by 4-bit windows equal the NAF ladder's."""
+    """k_combine_sigs' 64-bit G2 multiplications by 4-bit windows, 12-limb (curve.hpp) and digit
+    tower (g2d.hpp), equal the NAF ladder's."""
     hc.hc_g2_mul_u64_cmp.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
     rnd = random.Random(9)
     q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
-    for k in [1, 2, 15, 16, 17, 0xFFFFFFFFFFFFFFFF, 0xd201000000010000] + [rnd.getrandbits(64) for _ in range(6)]:
+    for k in [0, 1, 2, 15, 16, 17, 0x10, 0xF000000000000000, 0xFFFFFFFFFFFFFFFF, 0xd201000000010000] + [rnd.getrandbits(64) for _ in range(6)]:
         assert hc.hc_g2_mul_u64_cmp(q, k) == 1, hex(k)
+
+
+def test_g2d_add_special_cases(hc):
+    """k_combine_sigs' digit-tower G2 addition (g2d.hpp g2d_add) equals curve.hpp g2_add on general
+    Jacobian operands and on every special case (equal, opposite, identity operands), decided by
+    exact tests mod p; and fqd_is_zero_mod on unnormalised multiples of p."""
+    hc.hc_g2d_add_cases.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
+    assert hc.hc_fqd_is_zero_mod() == 1
+    rnd = random.Random(23)
+    for z0 in (1, 3, 0xFFFFFFFF12345678):
+        p = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+        q = bls.g2_compress(bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+        assert hc.hc_g2d_add_cases(p, q, z0) == 63
 
 
 def test_miller_gen_matches_mixed(hc):

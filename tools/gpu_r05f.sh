@@ -1,0 +1,19 @@
+# Round-5 iteration check: threshold + coin + broadcast-host GPU tests, the N=256 bench line with the
+# C4 round, the shard-of-8 slice, kernel stats.  Usage: gpurun -- bash tools/gpu_r05f.sh <tag>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+tag=${1:-r05f}
+bash tools/gpu_check.sh $tag "threshold or coin or host_api" || exit 1
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --configs=C4 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 gpurun_out/${tag}_bench.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/${tag}_bench.json')); c=d['configs']['C4']
+print('epoch', d['ms_per_step'], d['kernels_ms'], 'frac', d['roofline']['frac'], 'inflight', d.get('epochs_in_flight',{}).get('ms_per_epoch'))
+print('C4', c.get('round_ms_kernels'), c.get('round_ms_wall'), c.get('kernels_ms'))"
+timeout -k 10 300 python -u bench.py --shard-of 8 --no-cpu-baseline --configs= > gpurun_out/${tag}_bench_shard8.json 2> gpurun_out/${tag}_shard8.err || { echo "shard8 failed"; tail -20 gpurun_out/${tag}_shard8.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/${tag}_bench_shard8.json')); print('shard8', d['ms_per_step'], d['kernels_ms'], d.get('verify_lanes'))"
+cd /tmp && export TMPDIR=/tmp
+R="$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${tag}_prof" -o run -- python3 -u "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --in-flight 1 --configs=C4 > "$R/gpurun_out/${tag}_prof.log" 2>&1 || { echo "rocprof failed"; exit 1; }
+python3 "$R/tools/kstats.py" "$R/gpurun_out/${tag}_prof/run_results.db" > "$R/gpurun_out/${tag}_kernel_stats.txt" && head -30 "$R/gpurun_out/${tag}_kernel_stats.txt"
+echo done

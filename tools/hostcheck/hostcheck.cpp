@@ -5,6 +5,7 @@
 #include "../../hbbft_amd/csrc/pairing.hpp"
 #include "../../hbbft_amd/csrc/pairingd.hpp"
 #include "../../hbbft_amd/csrc/fe1d.hpp"
+#include "../../hbbft_amd/csrc/g2d.hpp"
 #include "../../hbbft_amd/csrc/hash.hpp"
 using namespace hbx;
 extern "C" {
@@ -195,11 +196,9 @@ int hc_fe1_step0_one(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, co
   s1_put_fq12d<1>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
   const bool one = fe1_step0<1, 1>(a, gf, gg);
   bool degenerate = false;
-  fe1_step_expmul<1, 1>(a, gt, gg, degenerate);
-  fe1_step_expmul<1, 1>(a, (uint32_t*)nullptr, gg, degenerate);
+  fe1_step12<1, 1>(a, gt, gg, degenerate);
   fe1_step34<1, 1>(a, gf, gt, gg, degenerate);
-  fe1_step5<1, 1>(a, gf, gg, degenerate);
-  const bool v = fq12d_is_one_seq(fe1_step6<1, 1>(a, gt, gg, degenerate));
+  const bool v = fq12d_is_one_seq(fe1_step56<1, 1>(a, gf, gt, degenerate));
   return (one ? 1 : 0) + (degenerate ? 2 : 0) + (v ? 4 : 0);
 }
 // digit-form product against the 12-limb one on canonical inputs: out = canonical a b (BE)
@@ -374,8 +373,57 @@ int hc_g2_mul_u64_cmp(const uint8_t* q96, uint64_t k) {
   g2a Q;
   if (g2_decompress(q96, Q) != HBX_PT_OK) return -1;
   const g2a a = g2_to_affine(g2_mul_u64_w4(Q, k)), b = g2_to_affine(g2_mul_u64_naf(Q, k));
-  if (a.inf || b.inf) return a.inf == b.inf ? 1 : 0;
-  return fq2_eq(a.x, b.x) && fq2_eq(a.y, b.y) ? 1 : 0;
+  // and the digit-tower multiplication (g2d.hpp, k_combine_sigs)
+  bool dinf;
+  const g2jd cd = g2d_mul_u64_w4(fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), k, dinf);
+  const g2a c = dinf ? g2_to_affine(g2_identity()) : g2_to_affine(g2jd_to_g2j(cd));
+  if (a.inf || b.inf || c.inf) return a.inf == b.inf && b.inf == c.inf ? 1 : 0;
+  return fq2_eq(a.x, b.x) && fq2_eq(a.y, b.y) && fq2_eq(a.x, c.x) && fq2_eq(a.y, c.y) ? 1 : 0;
+}
+// g2d_add (digit tower, exact special cases) against g2_add over the cases the combine's lane tree
+// can meet: P + Q, P + P, P + (-P), O + P, P + O, O + O, with the operands' Z scaled by z0
+// (Jacobian inputs, not only Z = 1).  Returns a bit mask of the cases that agree (63 = all).
+int hc_g2d_add_cases(const uint8_t* p96, const uint8_t* q96, uint64_t z0) {
+  g2a P, Q;
+  if (g2_decompress(p96, P) != HBX_PT_OK || g2_decompress(q96, Q) != HBX_PT_OK) return -1;
+  auto small = [](uint64_t v) {
+    fq a{};
+    a.l[0] = (uint32_t)v;
+    a.l[1] = (uint32_t)(v >> 32);
+    return fq_to_mont(a);
+  };
+  const fq2 z{small(z0), small(z0 + 7)};
+  auto jac = [&](const g2a& a, bool neg) {
+    const fq2 z2 = fq2_sqr(z);
+    const fq2 y = neg ? fq2_neg(a.y) : a.y;
+    return g2j{fq2_mul(a.x, z2), fq2_mul(fq2_mul(y, z2), z), z};
+  };
+  auto tod = [](const g2j& a) { return g2jd{fq2d_from_fq2(a.x), fq2d_from_fq2(a.y), fq2d_from_fq2(a.z)}; };
+  const g2j Pj = jac(P, false), Qj = g2_from_affine(Q), Pn = jac(P, true), O = g2_identity();
+  const g2j cases[6][2] = {{Pj, Qj}, {Pj, g2_from_affine(P)}, {Pj, Pn}, {O, Pj}, {Qj, O}, {O, O}};
+  int mask = 0;
+  for (int c = 0; c < 6; c++) {
+    const g2a want = g2_to_affine(g2_add(cases[c][0], cases[c][1]));
+    const g2a got = g2_to_affine(g2jd_to_g2j(g2d_add(tod(cases[c][0]), tod(cases[c][1]))));
+    const bool ok = want.inf || got.inf ? want.inf == got.inf : fq2_eq(want.x, got.x) && fq2_eq(want.y, got.y);
+    mask |= ok ? 1 << c : 0;
+  }
+  return mask;
+}
+// fqd_is_zero_mod over digit vectors of k p + e (k = -2..3, e = 0 or 1), unnormalised by moving
+// 2^28 between neighbouring digits: 1 if every answer is right.
+int hc_fqd_is_zero_mod() {
+  for (int k = -2; k <= 3; k++)
+    for (int e = 0; e <= 1; e++)
+      for (int sh = 0; sh < 13; sh++) {
+        fqd a;
+        for (int i = 0; i < 14; i++) a.d[i] = k * (int32_t)FQ_P28[i];
+        a.d[0] += e;
+        a.d[sh] += 1 << 28;
+        a.d[sh + 1] -= 1;
+        if (fqd_is_zero_mod(a) != (e == 0)) return 0;
+      }
+  return 1;
 }
 }
 extern "C" {
