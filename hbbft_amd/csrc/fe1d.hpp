@@ -234,7 +234,7 @@ HBX_HD fq12d fq12d_cyclotomic_sqr_seq(const fq12d& f) {
   return fq12d{fq6d{z0, z4, n3}, fq6d{n2, z1, z5}};
 }
 
-// ---- Karabina compressed squarings (the exp-by-|x| runs of 9, 32 and 16 squarings) ---------
+// ---- Karabina compressed squarings (the exp-by-|x| runs of 32 and 16 squarings) ---------------
 // An element of the cyclotomic subgroup is determined by four of its six Fq2 coefficients,
 // g1 = c0.c1, g2 = c0.c2, g3 = c1.c0, g5 = c1.c2, and its square's four from them with six Fq2
 // squarings (Granger-Scott: nine):
@@ -321,8 +321,10 @@ HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
 }
 
 // r^|x| with r's value also in slot a (the base): squaring runs between the one bits of |x| (63,
-// 62, 60, 57, 48, 16), a product by the base after each run but the last; the runs of 9, 32 and 16
-// squarings in compressed form.  If t3 is given, the value after the first run and product (r^3)
+// 62, 60, 57, 48, 16), a product by the base after each run but the last; the runs of 32 and 16
+// squarings in compressed form.  (A compressed squaring is ~7.1k VALU instructions against ~10.3k
+// for Granger-Scott, and a decompression ~38k, most of it the Fq inversion: the break-even run is
+// ~12 squarings, so the run of 9 stays uncompressed.)  If t3 is given, the value after the first run and product (r^3)
 // is stored there.  `degenerate`: see karabina_decompress.
 template <int S, int SG, class P, class PG>
 HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3, bool& degenerate) {
@@ -341,7 +343,7 @@ HBX_HD fq12d cyc_exp_abs_x_slot(fq12d r, P a, PG t3, bool& degenerate) {
 #pragma unroll 1
   for (int q = q0; q < 6; q++) {
     const int run = q == 0 ? 1 : q == 1 ? 2 : q == 2 ? 3 : q == 3 ? 9 : q == 4 ? 32 : 16;
-    if (q >= 3) {
+    if (q >= 4) {
       fq12c c{r.c0.c1, r.c0.c2, r.c1.c0, r.c1.c2};
 #pragma unroll 1
       for (int i = 0; i < run; i++) karabina_sqr(c);

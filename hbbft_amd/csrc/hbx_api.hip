@@ -90,9 +90,9 @@ struct hbx_ctx {
   dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
   dbuf fe1slot;  // one-lane checks: the final exponentiation's global slots F, T, G (fe1d.hpp)
   uint32_t force_fallback = 0;  // hbx_debug_force_fallback (tests only)
-  dbuf fb_lanes;                // u32: lanes the last one-lane launch's fallback check decided
+  dbuf fb_lanes;                // u32: checks the last one-lane / two-lane coin launch's fallback decided
   dbuf hs[6];                   // staging of the host-pointer broadcast calls
-  bool fb_lanes_valid = false;  // fb_lanes was reset by a one-lane launch
+  bool fb_lanes_valid = false;  // fb_lanes was reset by such a launch
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -1398,12 +1398,26 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
       const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
       if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
         return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
-      hipLaunchKernelGGL(k_verify_sig_shares2, dim3((n + 31) / 32, count), dim3(64), 0, s, c->coin_Hp.as<g2a>(),
-                         c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(), d_present, n,
-                         c->coin_valid.as<uint8_t>(), c->gslot.as<uint32_t>());
-      HIPCHK(c, hipGetLastError());
-      hipLaunchKernelGGL(k_verify_sig_shares2_fe, dim3((n + 31) / 32, count), dim3(64), 0, s, n,
-                         c->coin_valid.as<uint8_t>(), c->gslot.as<uint32_t>());
+      if (!c->fb_lanes.ensure(4)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
+      HIPCHK(c, hipMemsetAsync(c->fb_lanes.p, 0, 4, s));
+      c->fb_lanes_valid = true;
+      const dim3 grid((n + 31) / 32, count);
+      // Miller loops; the final exponentiation with compressed runs; then the pairs whose
+      // decompression met g3 = 0 (SHARE_FALLBACK) once more, Miller and Granger-Scott squarings
+      // only (both launches return at once per pair when there are none)
+      for (uint32_t retry = 0; retry < 2; retry++) {
+        hipLaunchKernelGGL(k_verify_sig_shares2, grid, dim3(64), 0, s, c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys,
+                           c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(), d_present, n, c->coin_valid.as<uint8_t>(),
+                           c->gslot.as<uint32_t>(), retry);
+        HIPCHK(c, hipGetLastError());
+        if (retry == 0)
+          hipLaunchKernelGGL(k_verify_sig_shares2_fe<true>, grid, dim3(64), 0, s, n, c->coin_valid.as<uint8_t>(),
+                             c->gslot.as<uint32_t>(), c->force_fallback, c->fb_lanes.as<uint32_t>());
+        else
+          hipLaunchKernelGGL(k_verify_sig_shares2_fe<false>, grid, dim3(64), 0, s, n, c->coin_valid.as<uint8_t>(),
+                             c->gslot.as<uint32_t>(), 0u, c->fb_lanes.as<uint32_t>());
+        HIPCHK(c, hipGetLastError());
+      }
     } else {
       hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
                          c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),

@@ -666,7 +666,8 @@ __global__ void __launch_bounds__(64) k_verify_shares2(const g1a* __restrict__ S
       const slot2<uint32_t*> G1{gb, 64u}, G2{gb + LDS_FQ6D_PACKED * 64, 64u};
       const uint32_t flags = (l1 ? 1u : 0u) | (skipA ? 0u : 2u) | (skipB ? 0u : 4u);
       check2d_miller(lines[j].h, sh, lines[j].w, pki, flags, (lds2)(reg + lane), B);
-      v = final_exp2d_is_one(A, B, G1, G2, l1);
+      bool dg = false;  // Granger-Scott squarings only: no decompression, never degenerate
+      v = final_exp2d_is_one<false>(A, B, G1, G2, l1, dg);
     }
   }
   if (!l1) {
@@ -693,7 +694,8 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
                                                            uint32_t n_keys, const g2a* __restrict__ sig,
                                                            const int32_t* __restrict__ sig_status,
                                                            const uint8_t* __restrict__ present, uint32_t n,
-                                                           uint8_t* __restrict__ valid, uint32_t* __restrict__ gslot) {
+                                                           uint8_t* __restrict__ valid, uint32_t* __restrict__ gslot,
+                                                           uint32_t retry) {
   __shared__ uint32_t region[LDS2_DWORDS * 64];
   const int lane = (int)(threadIdx.x & 63);
   const bool l1 = (lane & 1) != 0;
@@ -701,6 +703,8 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   const uint32_t inst = blockIdx.y;
   if (i >= n) return;  // whole pairs
   const size_t idx = (size_t)inst * n + i;
+  // retry: only the pairs k_verify_sig_shares2_fe<true> sent back (SHARE_FALLBACK), Miller again
+  if (retry && valid[idx] != SHARE_FALLBACK) return;  // pair-uniform
   const uint8_t res = share_precheck(sig_status[idx], present == nullptr || present[idx], i < n_keys, true);
   bool tf = true;
   if (res == HBX_SHARE_VALID) {
@@ -743,8 +747,14 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   const bool tf_pair = tf && tf_other != 0;
   if (!l1) valid[idx] = res != HBX_SHARE_VALID ? res : tf_pair ? SHARE_PENDING : (uint8_t)HBX_SHARE_UNDECODABLE;
 }
+// KARA: the final exponentiation's runs of 32 and 16 squarings compressed (pairing2d.hpp kara2);
+// a pair whose decompression meets g3 = 0 -- or every force_fallback-th share (tests only,
+// hbx_debug_force_fallback) -- becomes SHARE_FALLBACK and is counted in *fb; the host then runs
+// k_verify_sig_shares2 (retry) and k_verify_sig_shares2_fe<false> on those pairs alone.
+template <bool KARA>
 __global__ void __launch_bounds__(64) k_verify_sig_shares2_fe(uint32_t n, uint8_t* __restrict__ valid,
-                                                              uint32_t* __restrict__ gslot) {
+                                                              uint32_t* __restrict__ gslot, uint32_t force_fallback,
+                                                              uint32_t* __restrict__ fb) {
   __shared__ uint32_t region[LDS2_DWORDS * 64];
   const int lane = (int)(threadIdx.x & 63);
   const bool l1 = (lane & 1) != 0;
@@ -761,9 +771,19 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2_fe(uint32_t n, uint8_
 #pragma unroll 6
   for (int k = 0; k < LDS_FQ6D_PACKED; k++) B.half(h)[k * 64] = gb[h + k * 64];
   HBX_SEQ();
-  const bool v = final_exp2d_is_one(A, B, G1, G2, l1);
-  if (!l1) valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+  bool degenerate = KARA && force_fallback && (i % force_fallback) == 0;
+  const bool v = final_exp2d_is_one<KARA>(A, B, G1, G2, l1, degenerate);
+  if (!l1) {
+    if (KARA && degenerate) {
+      valid[idx] = SHARE_FALLBACK;
+      atomicAdd(fb, 1u);
+    } else {
+      valid[idx] = v ? HBX_SHARE_VALID : HBX_SHARE_INVALID;
+    }
+  }
 }
+template __global__ void k_verify_sig_shares2_fe<true>(uint32_t, uint8_t*, uint32_t*, uint32_t, uint32_t*);
+template __global__ void k_verify_sig_shares2_fe<false>(uint32_t, uint8_t*, uint32_t*, uint32_t, uint32_t*);
 #endif
 
 constexpr int COMBINE_THREADS = 256;
@@ -1646,9 +1666,9 @@ __device__ __forceinline__ g2j g2j_shfl_xor(const g2j& a, int m) {
 // G2.  Each S_k is in G2 (the decode checks membership), where psi acts as [x] = [-X]; with
 // lambda_k = d0 + d1 X + d2 X^2 + d3 X^3 (|d_i| < X < 2^64),
 //     lambda_k S_k = d0 S_k - d1 psi(S_k) + d2 psi^2(S_k) - d3 psi^3(S_k),
-// four independent 64-bit scalar multiplications, one per lane (lane 4k + i), instead of one
-// 255-bit multiplication: a quarter of the doubling chain; 4-bit fixed windows (g2_mul_u64_w4), so
-// the lanes' different digits do not serialise the additions.
+// four independent 64-bit scalar multiplications instead of one 255-bit multiplication: a quarter
+// of the doubling chain; 4-bit fixed windows (g2d.hpp g2d_mul_u64_w4), so the tasks' different
+// digits do not serialise the additions; the point arithmetic in the digit tower.
 //
 // B3 master check (PublicKey::verify(sig, nonce), common_coin.rs:196) in the same block, on its
 // last wave: every S_k was verified, e(pk_k, H) = e(g1, S_k), so by bilinearity
@@ -1673,8 +1693,10 @@ __global__ void __launch_bounds__(SIGCOMB_THREADS) k_combine_sigs(const uint8_t*
                                                                   uint8_t* __restrict__ master_ok,
                                                                   const g1a* __restrict__ g1tab) {
   // One block per instance: waves 0..2 the G2 combine (four psi-digit lanes per share), wave 3 the
-  // G1 master identity (two GLV lanes per share).  At t = 43 that is 172 + 86 tasks on 256 threads
-  // in ONE round of blocks (a block row per part made 512 one-wave-per-SIMD blocks, two rounds).
+  // G1 master identity (64 fixed-base window lanes).  At t = 43 that is 172 G2 tasks on 192 lanes
+  // in ONE round of blocks, one wave per SIMD.  (Lane pairs splitting every Fq2 product, g2d.hpp
+  // style, on 448 threads: 5.13 ms against 4.07 -- at two waves per SIMD the 256-VGPR budget
+  // spilled and the waves waited 57 % of their cycles.)
   constexpr int G2_THREADS = SIGCOMB_THREADS - 64;
   __shared__ uint16_t idx[COMBINE_MAX_T];
   __shared__ int s_count;

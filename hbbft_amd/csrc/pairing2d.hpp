@@ -30,6 +30,7 @@
 // Control flow is pair-uniform; every exchange reads the partner lane of the same pair.
 #pragma once
 #include "pairingd.hpp"
+#include "fe1d.hpp"
 #include "dpp.hpp"
 
 namespace hbx {
@@ -446,9 +447,57 @@ __device__ __forceinline__ void op_mul(const slot2<lds_u32*>& B, const slot2<P>&
   slot_put_fq6d(B.half(l1 ? 1 : 0), B.stride, fq6d_reduce(sel_t(co && l1, fq6d_neg(acc), acc)));
 }
 
-// B = B^(2^n) by cyclotomic squarings in registers
-__device__ __forceinline__ void op_sqr(const slot2<lds_u32*>& B, uint32_t n, bool l1) {
+// ---- Karabina compressed squarings on a pair (fe1d.hpp karabina_sqr split over the lanes) ----
+// fe1d.hpp's numbering: g1 = c0.c1, g2 = c0.c2, g3 = c1.c0, g5 = c1.c2 (lane 0 holds c0, lane 1
+// c1).  During a run lane 0 keeps (a, b) = (g3, g2) and lane 1 (g1, g5), and a squaring is ONE
+// lazily reduced Fq4 squaring per lane -- lane 0 (g3 + g2 Y)^2 = (p1, x23), lane 1 (g1 + g5 Y)^2 =
+// (p2, x15) -- plus an exchange of the two results (DPP):
+//   lane 0: g3' = 3 xi x15 + 2 g3,  g2' = 3 p2 - 2 g2;    lane 1: g1' = 3 p1 - 2 g1,  g5' = 3 x23 + 2 g5
+// (six convolutions and four reductions per lane against cyc_sqr2d's twelve and six).  A run ends
+// in one decompression (an Fq inversion, ~38k instructions), so only the runs of 32 and 16 use it.
+struct kara2 {
+  fq2d a, b;
+};
+__device__ __forceinline__ fq2d kara2_lin(const fq2d& a3, const fq2d& b2, bool minus) {  // reduce(3 a +/- 2 b)
+  const fq2d a = fq2d_add(fq2d_dbl(a3), a3);
+  const fq2d b = fq2d_dbl(b2);
+  return fq2d_reduce(sel_t(minus, fq2d_sub(a, b), fq2d_add(a, b)));
+}
+__device__ __forceinline__ kara2 kara2_sqr(const kara2& s, bool l1) {
+  fq2d P, X;
+  fq4d_sqr_lazy(s.a, s.b, P, X);
+  const fq2d Po = xchg_t(P), Xo = xchg_t(X);
+  const fq2d first = sel_t(l1, Po, fq2d_norm(fq2d_mul_xi(Xo)));
+  const fq2d second = sel_t(l1, Xo, Po);
+  return kara2{kara2_lin(first, s.a, l1), kara2_lin(second, s.b, !l1)};
+}
+// back to the split form: the pair swaps its coefficients, both lanes recover g4 and g0 (fe1d.hpp
+// karabina_decompress, the same values on both lanes), lane 0 keeps (g0, g1, g2), lane 1 (g3, g4,
+// g5).  `degenerate` (g3 = 0, the division impossible) is pair-uniform.
+__device__ __forceinline__ fq6d kara2_decompress(const kara2& s, bool l1, bool& degenerate) {
+  const fq2d oa = xchg_t(s.a), ob = xchg_t(s.b);
+  fq12c c;
+  c.g1 = sel_t(l1, s.a, oa);
+  c.g5 = sel_t(l1, s.b, ob);
+  c.g3 = sel_t(l1, oa, s.a);
+  c.g2 = sel_t(l1, ob, s.b);
+  const fq12d r = karabina_decompress(c, degenerate);
+  return sel_t(l1, r.c1, r.c0);
+}
+
+// B = B^(2^n) by cyclotomic squarings in registers: Granger-Scott, or compressed (KARA, n >= 16)
+template <bool KARA>
+__device__ __forceinline__ void op_sqr(const slot2<lds_u32*>& B, uint32_t n, bool l1, bool& degenerate) {
   lds_u32* mine = B.half(l1 ? 1 : 0);
+  if (KARA && n >= 16) {
+    // lane 0 takes g3 from lane 1 (its c0), lane 1 takes g1 from lane 0 (its c1); b = own c2
+    kara2 s{xchg_t(slot_get_fq2d(mine, B.stride, l1 ? 0 : 1)), slot_get_fq2d(mine, B.stride, 2)};
+#pragma unroll 1
+    for (uint32_t i = 0; i < n; i++) s = kara2_sqr(s, l1);
+    HBX_SEQ();
+    slot_put_fq6d(mine, B.stride, kara2_decompress(s, l1, degenerate));
+    return;
+  }
   fq6d r = slot_get_fq6d(mine, B.stride);
 #pragma unroll 1
   for (uint32_t i = 0; i < n; i++) r = cyc_sqr2d(r, l1);
@@ -579,10 +628,14 @@ __device__ __forceinline__ void op_inv(const slot2<lds_u32*>& A, const slot2<lds
   slot_put_fq6d(ao, A.stride, fq6d_reduce(conj2d(R, l1)));
 }
 
-// f^(3 (p^12 - 1)/r) == 1 with f (reduced) in B; A, G1, G2 as above.
+// f^(3 (p^12 - 1)/r) == 1 with f (reduced) in B; A, G1, G2 as above.  KARA: the runs of 32 and
+// 16 squarings compressed; `degenerate` is then set (pair-uniformly) when a decompression met
+// g3 = 0, and the verdict is not valid -- the caller decides that pair again with KARA = false.
 __device__ __forceinline__ bool is_one2d(const fq6d& A, bool l1);
+template <bool KARA>
 __device__ __forceinline__ bool final_exp2d_is_one(const slot2<lds_u32*>& A, const slot2<lds_u32*>& B,
-                                                  const slot2<uint32_t*>& G1, const slot2<uint32_t*>& G2, bool l1) {
+                                                  const slot2<uint32_t*>& G1, const slot2<uint32_t*>& G2, bool l1,
+                                                  bool& degenerate) {
   op_inv(A, B, l1);
 #pragma unroll 1
   for (int pc = 0; pc < FE2_STEPS; pc++) {
@@ -590,7 +643,7 @@ __device__ __forceinline__ bool final_exp2d_is_one(const slot2<lds_u32*>& A, con
     const uint32_t op = st & 15;
     HBX_SEQ();
     if (op == FE2_SQR) {
-      op_sqr(B, st >> 8, l1);
+      op_sqr<KARA>(B, st >> 8, l1, degenerate);
     } else if (op == FE2_MUL) {
       op_mul(B, A, ((st >> 4) & FE2_CX) != 0, ((st >> 4) & FE2_CO) != 0, l1);
     } else {

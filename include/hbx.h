@@ -149,16 +149,18 @@ int hbx_set_digest(hbx_ctx* ctx, int variant);
 int hbx_set_verify_lanes(hbx_ctx* ctx, int lanes);
 /* Lanes per check the last decryption-share launch used (1, 2, 3, 6 or 7; 0 before any launch). */
 int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
-/* Tests only: in one-lane checks, treat the lane of every `every`-th sender (0 = none, the default)
- * as if its compressed squarings had met a zero denominator, so the single-kernel fallback check
- * decides it.  Results are unchanged.  (Real inputs reach that path only through an element with a
- * zero Fq2 coefficient at the end of a compressed run, ~2^-760 for values nobody chose; the one
- * degenerate start a proposer can choose -- a ciphertext with r = 3(x^2 - 1), for which every honest
- * share's check is 1 after the easy part -- is decided by the first step without a fallback.) */
+/* Tests only: in one-lane decryption-share checks and two-lane coin checks, treat the check of
+ * every `every`-th sender (0 = none, the default) as if its compressed squarings had met a zero
+ * denominator, so the fallback path decides it (the single-kernel one-lane check; for the coin, the
+ * pair's Miller loop again and a final exponentiation without compressed runs).  Results are
+ * unchanged.  (Real inputs reach that path only through an element with a zero Fq2 coefficient at
+ * the end of a compressed run, ~2^-760 for values nobody chose; the one degenerate start a proposer
+ * can choose -- a ciphertext with r = 3(x^2 - 1), for which every honest share's check is 1 after
+ * the easy part -- is decided by the first step without a fallback.) */
 int hbx_debug_force_fallback(hbx_ctx* ctx, uint32_t every);
-/* Lanes of the last one-lane decryption-share launch that the single-kernel fallback check decided
- * (0 unless hbx_debug_force_fallback is on); waits for the launch.  Diagnostics: no reference
- * counterpart. */
+/* Checks of the last one-lane decryption-share launch, or of the last two-lane coin launch, that the
+ * fallback path decided (0 unless hbx_debug_force_fallback is on); waits for the launch.
+ * Diagnostics: no reference counterpart. */
 int64_t hbx_get_fallback_lanes(hbx_ctx* ctx);
 /* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
  * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over

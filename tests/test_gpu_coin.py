@@ -53,6 +53,30 @@ def test_coin_matches_golden(hbx_ctx, n, lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [7, 128])
+def test_two_lane_coin_fallback_matches_golden(hbx_ctx, n):
+    """The two-lane coin check's fallback: a pair whose compressed squarings meet g3 = 0 (forced
+    here for every third sender) is sent back -- Miller loop again, final exponentiation without
+    compressed runs -- and decided with the same statuses as the fixture."""
+    d = _load(n)
+    _digest(hbx_ctx, d)
+    hbx_ctx.set_verify_lanes(2)
+    assert (hbx_ctx.set_pk_shares([r.tobytes() for r in d["pk_comp"]]) == 0).all()
+    hbx_ctx.prepare_nonces(_nonces(d))
+    hbx_ctx.debug_force_fallback(3)
+    try:
+        valid = hbx_ctx.verify_sig_shares(d["sigs"], d["present"])
+        assert hbx_ctx.fallback_lanes() > 0
+    finally:
+        hbx_ctx.debug_force_fallback(0)
+    np.testing.assert_array_equal(valid, d["expect_valid"])
+    count, nn = d["sigs"].shape[:2]
+    np.testing.assert_array_equal(hbx_ctx.sig_share_status(count, nn), d["expect_share_status"])
+    hbx_ctx.verify_sig_shares(d["sigs"], d["present"])
+    assert hbx_ctx.fallback_lanes() == 0  # nothing reaches the fallback unforced
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [4, 128, "coin_n4_sha3"])
 def test_sign_matches_honest_shares(hbx_ctx, n):
     d = _load(n)
