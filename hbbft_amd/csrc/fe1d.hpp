@@ -127,46 +127,7 @@ HBX_HD void s1_copy(PD d, PS s) {
   }
 }
 
-HBX_HD fq6d fq6d_zero_() {
-  const fqd z = fqd_zero();
-  return fq6d{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
-}
-
-// acc += a * y (fieldd.hpp fq6d_mul's Karatsuba), y(q) its Fq2 coefficient q, every Fq2 product
-// folded into the accumulator at once, a fence between products (HBX_SEQ); a and y normalised,
-// acc normalised (or zero) on entry; carry-normalised on exit.  The digit sums stay below 2^31:
-// acc + 7 terms of at most two normalised values each.
-template <class Y>
-HBX_HD void fq6d_mul_acc1(fq6d& acc, const fq6d& a, Y y) {
-  {
-    const fq2d t0 = fq2d_mul(a.c0, y(0));
-    acc.c0 = fq2d_add(acc.c0, t0);
-    acc.c1 = fq2d_sub(acc.c1, t0);
-    acc.c2 = fq2d_sub(acc.c2, t0);
-  }
-  HBX_SEQ();
-  {
-    const fq2d t1 = fq2d_mul(a.c1, y(1));
-    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
-    acc.c1 = fq2d_sub(acc.c1, t1);
-    acc.c2 = fq2d_add(acc.c2, t1);
-  }
-  HBX_SEQ();
-  {
-    const fq2d t2 = fq2d_mul(a.c2, y(2));
-    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
-    acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
-    acc.c2 = fq2d_sub(acc.c2, t2);
-  }
-  HBX_SEQ();
-  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))));
-  HBX_SEQ();
-  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))));
-  HBX_SEQ();
-  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))));
-  HBX_SEQ();
-  acc = fq6d_norm(acc);
-}
+// fq6d_zero_ and fq6d_mul_acc1 (acc += a * y, y streamed): pairingd.hpp
 
 // X * Y, X in registers (reduced, or its conjugate), Y the packed value in slot y.  Reduced.
 // Karatsuba over w: c0 = X0 Y0 + v X1 Y1, c1 = (X0 + X1)(Y0 + Y1) - X0 Y0 - X1 Y1.
@@ -466,37 +427,46 @@ HBX_HD fq6d s1_get_half(PG p, int h) {
 // fe1_easy_first restated over the slots with at most two Fq6 values in registers at a time (the
 // round-4 version held f's halves beside an Fq12 squaring: 224 spilled VGPRs, 0.46 GB of scratch
 // traffic per N=256 launch).  With A = f0^2, B = v f1^2, C = f0 f1 (three Fq6 products, each
-// streaming its second operand from slot F): N(f) = A - B, conj(f)^2 = (A + B) - 2 C w, and
-// t0 = conj(f)^2 / N(f) -- three Fq6 products for N(f) and conj(f)^2 instead of four.  Slot a
-// holds v f1^2 (words 78..155), then N^-1 (words 0..77); slot G's half 0 holds A + B until t0's
-// first half is formed.
+// streaming its second operand from the lane's LDS slot): N(f) = A - B, conj(f)^2 = (A + B) -
+// 2 C w, and t0 = conj(f)^2 / N(f) -- three Fq6 products for N(f) and conj(f)^2 instead of four.
+// f is copied into slot a first, so the products stream it from LDS (streamed from slot F in
+// global memory, every Fq2 operand read behind a fence exposed a global load's latency: the step
+// waited 29 % of its cycles); B and C wait in slot T's halves (free until F1 writes t^3), A + B in
+// slot G's half 0, and N^-1 replaces f in slot a once the three products are done.
 template <int S, int SG, class P, class PG>
-HBX_HD bool fe1_step0(P a, PG gf, PG gg) {
+HBX_HD bool fe1_step0(P a, PG gf, PG gt, PG gg) {
+  s1_copy<S, SG>(a, gf);
+  HBX_SEQ();
   {
-    // B = v f1^2 -> slot a words 78..155
+    // B = v f1^2 -> slot T half 0
     fq6d B = fq6d_zero_();
-    {
-      const fq6d f1 = s1_get_half<SG>(gf, 1);
-      fq6d_mul_acc1(B, f1, [&](int q) { return s1_get_fq2d<SG>(gf, 3 + q); });
-    }
+    fq6d_mul_acc1(B, s1_get_half<S>(a, 1), [&](int q) { return s1_get_fq2d<S>(a, 3 + q); });
     B = fq6d_norm(fq6d_mul_v(B));
-    s1_put_fq2d<S>(a, 3, B.c0);
-    s1_put_fq2d<S>(a, 4, B.c1);
-    s1_put_fq2d<S>(a, 5, B.c2);
+    s1_put_fq2d<SG>(gt, 0, B.c0);
+    s1_put_fq2d<SG>(gt, 1, B.c1);
+    s1_put_fq2d<SG>(gt, 2, B.c2);
   }
   HBX_SEQ();
   {
-    // A = f0^2; N = A - B (kept), A + B -> slot G half 0
+    // C' = -2 f0 f1 -> slot T half 1
+    fq6d C = fq6d_zero_();
+    fq6d_mul_acc1(C, s1_get_half<S>(a, 0), [&](int q) { return s1_get_fq2d<S>(a, 3 + q); });
+    C = fq6d_reduce(fq6d_neg(fq6d_add(C, C)));
+    s1_put_fq2d<SG>(gt, 3, C.c0);
+    s1_put_fq2d<SG>(gt, 4, C.c1);
+    s1_put_fq2d<SG>(gt, 5, C.c2);
+  }
+  HBX_SEQ();
+  {
+    // A = f0^2; N = A - B (kept), A + B -> slot G half 0; N^-1 -> slot a words [0, 78) (f is
+    // no longer needed)
     fq6d A = fq6d_zero_();
-    {
-      const fq6d f0 = s1_get_half<SG>(gf, 0);
-      fq6d_mul_acc1(A, f0, [&](int q) { return s1_get_fq2d<SG>(gf, q); });
-    }
+    fq6d_mul_acc1(A, s1_get_half<S>(a, 0), [&](int q) { return s1_get_fq2d<S>(a, q); });
     HBX_SEQ();
     fq6d n;
 #pragma unroll 1
-    for (int q = 0; q < 3; q++) {  // one Fq2 coefficient at a time (B from the slot)
-      const fq2d b = s1_get_fq2d<S>(a, 3 + q);
+    for (int q = 0; q < 3; q++) {  // one Fq2 coefficient at a time (B from slot T)
+      const fq2d b = s1_get_fq2d<SG>(gt, q);
       const fq2d aq = q == 0 ? A.c0 : q == 1 ? A.c1 : A.c2;
       s1_put_fq2d<SG>(gg, q, fq2d_reduce(fq2d_add(aq, b)));
       const fq2d nq = fq2d_reduce(fq2d_sub(aq, b));
@@ -510,16 +480,9 @@ HBX_HD bool fe1_step0(P a, PG gf, PG gg) {
   HBX_SEQ();
   fq12d r;
   {
-    // t0.c1 = -2 C N^-1, C = f0 f1
-    fq6d C = fq6d_zero_();
-    {
-      const fq6d f0 = s1_get_half<SG>(gf, 0);
-      fq6d_mul_acc1(C, f0, [&](int q) { return s1_get_fq2d<SG>(gf, 3 + q); });
-    }
-    C = fq6d_reduce(fq6d_neg(fq6d_add(C, C)));
-    HBX_SEQ();
+    // t0.c1 = -2 C N^-1
     fq6d T1 = fq6d_zero_();
-    fq6d_mul_acc1(T1, C, [&](int q) { return s1_get_fq2d<S>(a, q); });
+    fq6d_mul_acc1(T1, s1_get_half<SG>(gt, 1), [&](int q) { return s1_get_fq2d<S>(a, q); });
     r.c1 = fq6d_reduce(T1);
   }
   HBX_SEQ();
@@ -607,7 +570,7 @@ HBX_HD fq12d fe1_step56(P a, PG gf, PG gt, bool& degenerate) {
 // the whole chain on one lane (host checks; the kernels run one step each)
 template <int S, int SG, class P, class PG>
 HBX_HD fq12d fe1_chain(P a, PG gf, PG gt, PG gg, bool& degenerate) {
-  fe1_step0<S, SG>(a, gf, gg);
+  fe1_step0<S, SG>(a, gf, gt, gg);
   fe1_step12<S, SG>(a, gt, gg, degenerate);
   fe1_step34<S, SG>(a, gf, gt, gg, degenerate);
   return fe1_step56<S, SG>(a, gf, gt, degenerate);

@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
   // takes the degenerate path, so the fallback check is exercised
   bool degenerate = STEP == 1 && force_fallback && (i % force_fallback) == 0;
   if (STEP == 0) {
-    if (fe1_step0<64, 64>(a, gf, gg)) {  // t = 1 after the easy part: the check holds (fe1d.hpp)
+    if (fe1_step0<64, 64>(a, gf, gt, gg)) {  // t = 1 after the easy part: the check holds (fe1d.hpp)
       valid[idx] = HBX_SHARE_VALID;
       if (i == me && ct_valid) ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : HBX_CT_VALID;
       return;

@@ -220,18 +220,98 @@ HBX_HD fq12d miller_loop2_parked_d(const line_pre_d* LA, bool useA, const line_p
   return fq12d_conj(f);
 }
 
+HBX_HD fq6d fq6d_zero_() {
+  const fqd z = fqd_zero();
+  return fq6d{fq2d{z, z}, fq2d{z, z}, fq2d{z, z}};
+}
+
+// acc += a * y (fieldd.hpp fq6d_mul's Karatsuba), y(q) its Fq2 coefficient q, every Fq2 product
+// folded into the accumulator at once, a fence between products (HBX_SEQ); a and y normalised,
+// acc normalised (or zero) on entry; carry-normalised on exit.  The digit sums stay below 2^31:
+// acc + 7 terms of at most two normalised values each.
+template <class Y>
+HBX_HD void fq6d_mul_acc1(fq6d& acc, const fq6d& a, Y y) {
+  {
+    const fq2d t0 = fq2d_mul(a.c0, y(0));
+    acc.c0 = fq2d_add(acc.c0, t0);
+    acc.c1 = fq2d_sub(acc.c1, t0);
+    acc.c2 = fq2d_sub(acc.c2, t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(a.c1, y(1));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
+    acc.c1 = fq2d_sub(acc.c1, t1);
+    acc.c2 = fq2d_add(acc.c2, t1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t2 = fq2d_mul(a.c2, y(2));
+    acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
+    acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
+    acc.c2 = fq2d_sub(acc.c2, t2);
+  }
+  HBX_SEQ();
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))));
+  HBX_SEQ();
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))));
+  HBX_SEQ();
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))));
+  HBX_SEQ();
+  acc = fq6d_norm(acc);
+}
+
+// Slot words of the scaled Miller loop (word k at park[k * LDS_FQ12_STRIDE]): 0..55 the points'
+// scalars (park_scaled_points), 56..139 an Fq6 operand streamed into a product (below).
+constexpr int ML_PARK_Y = 56;
+HBX_HD void park_put_fq2d(lds_u32* park, int word, const fq2d& a) {
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    park[(word + i) * LDS_FQ12_STRIDE] = (uint32_t)a.c0.d[i];
+    park[(word + 14 + i) * LDS_FQ12_STRIDE] = (uint32_t)a.c1.d[i];
+  }
+}
+HBX_HD fq2d park_get_fq2d(const lds_u32* park, int word) {
+  fq2d a;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    a.c0.d[i] = (int32_t)park[(word + i) * LDS_FQ12_STRIDE];
+    a.c1.d[i] = (int32_t)park[(word + 14 + i) * LDS_FQ12_STRIDE];
+  }
+  return a;
+}
+// f^2 (fieldd.hpp fq12d_sqr: c0 = (a0 + a1)(a0 + v a1) - ab - v ab, c1 = 2 ab) with the operand
+// a0 + v a1 parked in the slot and streamed into its product, one Fq2 coefficient per read: 84
+// registers fewer at the squaring's peak, where the loop spilled into AGPRs (~6 % of its
+// instructions were accvgpr moves).  The same element.
+HBX_HD fq12d fq12d_sqr_parked(const fq12d& a, lds_u32* park) {
+  {
+    const fq6d y = fq6d_norm(fq6d_add(a.c0, fq6d_mul_v(a.c1)));
+    park_put_fq2d(park, ML_PARK_Y, y.c0);
+    park_put_fq2d(park, ML_PARK_Y + 28, y.c1);
+    park_put_fq2d(park, ML_PARK_Y + 56, y.c2);
+  }
+  HBX_SEQ();
+  fq6d ab = fq6d_zero_();
+  fq6d_mul_acc1(ab, a.c0, [&](int q) { return q == 0 ? a.c1.c0 : q == 1 ? a.c1.c1 : a.c1.c2; });
+  HBX_SEQ();
+  fq6d t = fq6d_zero_();
+  fq6d_mul_acc1(t, fq6d_norm(fq6d_add(a.c0, a.c1)), [&](int q) { return park_get_fq2d(park, ML_PARK_Y + 28 * q); });
+  return fq12d{fq6d_reduce(fq6d_sub(fq6d_sub(t, ab), fq6d_mul_v(ab))), fq6d_reduce(fq6d_add(ab, ab))};
+}
+
 // miller_loop2_parked_d over lines divided by y_P: the slot holds (x_A / y_A, 1 / y_A,
 // x_B / y_B, 1 / y_B) (park_scaled_points), each line becomes (c0 / y) + (c1 x / y) v + v w and its
 // product costs two Fq-by-Fq2 products for the scaled coefficients instead of one plus the three
 // of the c4 = y term (fq12d_mul_by_01v).  The element differs from miller_loop2_parked_d's by a
 // product of Fq factors (1 / y per line), which the final exponentiation maps to 1: the same verdict.
 HBX_HD fq12d miller_loop2_scaled_d(const line_pre_d* LA, bool useA, const line_pre_d* LB, bool useB,
-                                   const lds_u32* park) {
+                                   lds_u32* park) {
   fq12d f = fq12d_one();
   int k = 0;
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    if (i != 62) f = fq12d_sqr(f);
+    if (i != 62) f = fq12d_sqr_parked(f, park);
     const int steps = ((BLS_X >> i) & 1) ? 4 : 2;  // (A, B) lines of the doubling [+ addition]
 #pragma unroll 1
     for (int s = 0; s < steps; s++) {

@@ -194,7 +194,7 @@ int hc_fe1_step0_one(const uint8_t* pa, const uint8_t* qa, const uint8_t* pb, co
                                   fqd_from_fq(PB.y), true);
   static uint32_t a[FE1_WORDS], gf[FE1_WORDS], gt[FE1_WORDS], gg[FE1_WORDS];
   s1_put_fq12d<1>(gf, fq12d{fd.c0, fq6d_norm(fd.c1)});
-  const bool one = fe1_step0<1, 1>(a, gf, gg);
+  const bool one = fe1_step0<1, 1>(a, gf, gt, gg);
   bool degenerate = false;
   fe1_step12<1, 1>(a, gt, gg, degenerate);
   fe1_step34<1, 1>(a, gf, gt, gg, degenerate);
