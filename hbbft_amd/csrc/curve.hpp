@@ -248,7 +248,9 @@ HBX_HDNI bool g1_is_torsion_free(const g1a& P) {
 }
 
 // zcash compressed G1 -> affine (Montgomery).  No subgroup check.
-HBX_HDNI int32_t g1_decompress(const uint8_t* b48, g1a& out) {
+// `sqrt(a, y)`: a square root of a, false if none (fq_sqrt; g1d.hpp passes the digit-tower one).
+template <class Sqrt>
+HBX_HD int32_t g1_decompress_t(const uint8_t* b48, g1a& out, Sqrt sqrt) {
   const uint8_t flags = b48[0];
   out.inf = false;
   if (!(flags & 0x80)) return HBX_PT_BAD_FLAGS;
@@ -269,11 +271,14 @@ HBX_HDNI int32_t g1_decompress(const uint8_t* b48, g1a& out) {
   const fq x = fq_to_mont(xc);
   const fq rhs = fq_add(fq_mul(fq_sqr(x), x), fq_from_const(FQ_B1));
   fq y;
-  if (!fq_sqrt(rhs, y)) return HBX_PT_NOT_ON_CURVE;
+  if (!sqrt(rhs, y)) return HBX_PT_NOT_ON_CURVE;
   if (fq_lex_largest(y) != ((flags & 0x20) != 0)) y = fq_neg(y);
   out.x = x;
   out.y = y;
   return HBX_PT_OK;
+}
+HBX_HDNI int32_t g1_decompress(const uint8_t* b48, g1a& out) {
+  return g1_decompress_t(b48, out, [](const fq& a, fq& y) { return fq_sqrt(a, y); });
 }
 
 HBX_HD void g1_compress(const g1a& p, uint8_t* b48) {

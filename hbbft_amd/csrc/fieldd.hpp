@@ -156,6 +156,23 @@ HBX_HD fqd fqd_reduce(const fqd& a) {
   return r;
 }
 
+// One parallel carry step ("relaxed" form for latency-bound chains: groupd.hpp, g1d.hpp):
+// d_i <- (d_i mod 2^28) + floor(d_(i-1) / 2^28), the top digit keeps the rest.  Input digits below
+// 2^31 in magnitude; output digits in (-2^28 - 8, 2^28 + 8); the value is unchanged.  Three VALU
+// levels, against fqd_norm's 13-step carry chain.
+HBX_HD fqd fqd_relax(const fqd& a) {
+  fqd r;
+  r.d[0] = a.d[0] & DMASK;
+  HBX_LAUNDER(r.d[0]);
+#pragma unroll
+  for (int i = 1; i < 13; i++) {
+    r.d[i] = (a.d[i] & DMASK) + (a.d[i - 1] >> 28);
+    HBX_LAUNDER(r.d[i]);
+  }
+  r.d[13] = a.d[13] + (a.d[12] >> 28);
+  return r;
+}
+
 // Montgomery product a b / 2^392 (signed digits; see the bounds above).  Column k of the digit
 // convolution accumulates in int64 (v_mad_i64_i32), the reduction digits m_k = -acc p^-1 mod 2^28
 // in unsigned (v_mad_u64_u32); three a*b and two m*p chains per column for ILP, as fq_mul_body.
@@ -350,6 +367,7 @@ HBX_HD fq2d fq2d_dbl(const fq2d& a) { return fq2d{fqd_dbl(a.c0), fqd_dbl(a.c1)};
 HBX_HD fq2d fq2d_conj(const fq2d& a) { return fq2d{a.c0, fqd_neg(a.c1)}; }
 HBX_HD fq2d fq2d_norm(const fq2d& a) { return fq2d{fqd_norm(a.c0), fqd_norm(a.c1)}; }
 HBX_HD fq2d fq2d_reduce(const fq2d& a) { return fq2d{fqd_reduce(a.c0), fqd_reduce(a.c1)}; }
+HBX_HD fq2d fq2d_relax(const fq2d& a) { return fq2d{fqd_relax(a.c0), fqd_relax(a.c1)}; }
 // times xi = 1 + u
 HBX_HD fq2d fq2d_mul_xi(const fq2d& a) { return fq2d{fqd_sub(a.c0, a.c1), fqd_add(a.c0, a.c1)}; }
 

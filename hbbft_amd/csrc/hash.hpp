@@ -12,6 +12,7 @@
 #include "curve.hpp"
 #include "fieldd.hpp"
 #include "dpp.hpp"
+#include "groupd.hpp"
 
 namespace hbx {
 
@@ -349,12 +350,23 @@ __device__ __forceinline__ fq fq_sel16(int s, const fq (&v)[16]) {
   return r;
 }
 
+#ifndef HBX_DBL_MARK
+#define HBX_DBL_MARK(k)  // timing hooks (tools/microbench/dblstamp.hip: clock stamps between the
+#define HBX_DBL_USE(v)   // segments; USE pins a product's result before the next stamp)
+#endif
 __device__ __forceinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
   const int s = gl & 7;
   const fq x0 = p.x.c0, x1 = p.x.c1, y0 = p.y.c0, y1 = p.y.c1, z0 = p.z.c0, z1 = p.z.c1;
   // round 1: A = X^2 (lanes 0, 1), B = Y^2 (2, 3), Y Z (4..7)
-  fq r = fq_mul_inl(fq_sel8(s, fq_add(x0, x1), x0, fq_add(y0, y1), y0, y0, y1, y0, y1),
-                fq_sel8(s, fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, z0, z1, z1, z0));
+  HBX_DBL_MARK(0);
+  const fq a1 = fq_sel8(s, fq_add(x0, x1), x0, fq_add(y0, y1), y0, y0, y1, y0, y1);
+  const fq b1 = fq_sel8(s, fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, z0, z1, z1, z0);
+  HBX_DBL_USE(a1);
+  HBX_DBL_USE(b1);
+  HBX_DBL_MARK(1);
+  fq r = fq_mul_inl(a1, b1);
+  HBX_DBL_USE(r);
+  HBX_DBL_MARK(2);
   const fq2 A = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
   const fq2 B = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
   const fq2 YZ = fq2{fq_sub(fq_from_row<4>(r), fq_from_row<5>(r)),
@@ -362,8 +374,14 @@ __device__ __forceinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
   // round 2: C = B^2 (0, 1), T = (X + B)^2 (2, 3), F = E^2 with E = 3A (4, 5)
   const fq2 S = fq2_add(p.x, B);
   const fq2 E = fq2_add(fq2_dbl(A), A);
-  r = fq_mul_inl(fq_sel8(s, fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0, E.c0, E.c0),
-             fq_sel8(s, fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1, E.c1, E.c1));
+  const fq a2 = fq_sel8(s, fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0, E.c0, E.c0);
+  const fq b2 = fq_sel8(s, fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1, E.c1, E.c1);
+  HBX_DBL_USE(a2);
+  HBX_DBL_USE(b2);
+  HBX_DBL_MARK(3);
+  r = fq_mul_inl(a2, b2);
+  HBX_DBL_USE(r);
+  HBX_DBL_MARK(4);
   const fq2 C = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
   const fq2 T = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
   const fq2 F = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
@@ -371,12 +389,26 @@ __device__ __forceinline__ g2j g2_dbl_group(const g2j& p, int gl, int gbase) {
   const fq2 X3 = fq2_sub(F, fq2_dbl(D));
   // round 3: E (D - X3) (0..3)
   const fq2 G = fq2_sub(D, X3);
-  r = fq_mul_inl(fq_sel8(s, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1),
-             fq_sel8(s, G.c0, G.c1, G.c1, G.c0, G.c0, G.c1, G.c1, G.c0));
+  const fq a3 = fq_sel8(s, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1);
+  const fq b3 = fq_sel8(s, G.c0, G.c1, G.c1, G.c0, G.c0, G.c1, G.c1, G.c0);
+  HBX_DBL_USE(a3);
+  HBX_DBL_USE(b3);
+  HBX_DBL_MARK(5);
+  r = fq_mul_inl(a3, b3);
+  HBX_DBL_USE(r);
+  HBX_DBL_MARK(6);
   const fq2 EG = fq2{fq_sub(fq_from_row<0>(r), fq_from_row<1>(r)),
                      fq_add(fq_from_row<2>(r), fq_from_row<3>(r))};
   const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
-  return g2j{X3, fq2_sub(EG, C8), fq2_dbl(YZ)};
+  const g2j out{X3, fq2_sub(EG, C8), fq2_dbl(YZ)};
+  HBX_DBL_USE(out.x.c0);
+  HBX_DBL_USE(out.x.c1);
+  HBX_DBL_USE(out.y.c0);
+  HBX_DBL_USE(out.y.c1);
+  HBX_DBL_USE(out.z.c0);
+  HBX_DBL_USE(out.z.c1);
+  HBX_DBL_MARK(7);
+  return out;
 }
 __device__ __forceinline__ g2j g2_dbl_n_group(g2j p, int n, int gl, int gbase) {
   for (int i = 0; i < n; i++) p = g2_dbl_group(p, gl, gbase);
@@ -525,6 +557,9 @@ __device__ g2j g2_clear_cofactor_group(const g2j& P, int gl, int gbase, bool ful
 // clearing.  A cleared point equal to the identity makes the sequential loop continue with the next
 // candidate; so does this one (base = winner + 1).  `active` must be group-uniform.
 // Returns true on the lane that holds the result in `out`.
+#ifndef HBX_HASH_GROUPD
+#define HBX_HASH_GROUPD 1  // 1: the cofactor clearing in the digit tower (groupd.hpp), 0: 12-limb rounds
+#endif
 #ifndef HBX_PHASE
 #define HBX_PHASE(k)  // profiling hook (tools/microbench/hashg2.hip records wall-clock stamps)
 #endif
@@ -576,7 +611,14 @@ __device__ bool hash_g2_group(const uint8_t* d32, bool active, g2j& out, bool fu
     const int src = gbase + win;
     const fq2 xw = fq2{fq_from_lane(x.c0, src), fq_from_lane(x.c1, src)};
     const fq2 yw = fq2{fq_from_lane(y.c0, src), fq_from_lane(y.c1, src)};
+#if HBX_HASH_GROUPD
+    {
+      const fq2d one{fqd_const(FQD_ONE), fqd_zero()};
+      out = g2jd_to_g2j(g2d_clear_cofactor_group(g2jd{fq2d_from_fq2(xw), fq2d_from_fq2(yw), one}, gl, full));
+    }
+#else
     out = g2_clear_cofactor_group(g2j{xw, yw, fq2_one()}, gl, gbase, full);
+#endif
     HBX_PHASE(4);
     const bool ident = g2j_is_identity(out);
     if ((__ballot(ident) & gmask) == 0) return gl == win;

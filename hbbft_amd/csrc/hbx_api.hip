@@ -686,7 +686,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     const bool grouped = senders ? ((size_t)p * senders + 63) / 64 < (size_t)VERIFY_FILL_WAVES : p <= 64;
     auto kpl = grouped ? k_prepare_lines<true> : k_prepare_lines<false>;
     hipLaunchKernelGGL(kpl, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
-                       c->lines.as<line_pre>(), c->scratch.as<fq2>(), c->dec_st.as<int32_t>(), p,
+                       c->lines_d.as<line_pre_d>(), c->scratch.as<fq2d>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
                        own ? c->own_S.as<g1a>() : nullptr, early_n, me_early,
                        own_entry ? c->S.as<g1a>() : nullptr, own_entry ? c->S_status.as<int32_t>() : nullptr,
@@ -694,7 +694,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = 2 * p * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), b64, 0, s, c->lines.as<line_pre>(),
-                       c->scratch.as<fq2>(), nl, c->lines_d.as<line_pre_d>(), c->G2pts.as<g2a>(),
+                       c->scratch.as<fq2d>(), nl, c->lines_d.as<line_pre_d>(), c->G2pts.as<g2a>(),
                        c->Hj.as<g2j>());
   }
   HIPCHK(c, hipGetLastError());
@@ -1379,12 +1379,12 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
     // H''s prepared lines for the one-lane kernel (wave-uniform loads)
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
-                       c->coin_lines.as<line_pre>(), c->coin_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
+                       c->coin_lines_d.as<line_pre_d>(), c->coin_scratch.as<fq2d>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                        UINT32_MAX, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     const uint32_t nl = count * MILLER_LINES;
     hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->coin_lines.as<line_pre>(),
-                       c->coin_scratch.as<fq2>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
+                       c->coin_scratch.as<fq2d>(), nl, c->coin_lines_d.as<line_pre_d>(), nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
     c->coin_lines_ready = true;
     // the lines are built on this call's stream: move the prepare event past them, so a later
@@ -1507,12 +1507,12 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
                      c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(), 1u);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
-                     c->vs_lines.as<line_pre>(), c->vs_scratch.as<fq2>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
+                     c->vs_lines_d.as<line_pre_d>(), c->vs_scratch.as<fq2d>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                      UINT32_MAX, nullptr, nullptr, nullptr);
   HIPCHK(c, hipGetLastError());
   const uint32_t nl = count * MILLER_LINES;
   hipLaunchKernelGGL(k_normalise_lines, dim3((nl + 63) / 64), dim3(64), 0, s, c->vs_lines.as<line_pre>(),
-                     c->vs_scratch.as<fq2>(), nl, c->vs_lines_d.as<line_pre_d>(), nullptr, nullptr);
+                     c->vs_scratch.as<fq2d>(), nl, c->vs_lines_d.as<line_pre_d>(), nullptr, nullptr);
   HIPCHK(c, hipGetLastError());
   {
     timed t_(c, HBX_K_VERIFY_SIG, s);

@@ -21,6 +21,7 @@
 #include "pairing2d.hpp"
 #include "fe1d.hpp"
 #include "g2d.hpp"
+#include "g1d.hpp"
 #include "curve4.hpp"
 #include "wide.hpp"
 
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(64) k_decompress_g1(const uint8_t* __restrict_
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1a p;
-  const int32_t st = g1_decompress(comp + (size_t)i * 48, p);
+  const int32_t st = g1_decompress_d(comp + (size_t)i * 48, p);
   out[i] = p;
   status[i] = st;
 }
@@ -133,8 +134,8 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
     const size_t i = (size_t)(bid - hash_blocks - dec_blocks) * blockDim.x + threadIdx.x;
     if (i >= share_count || (uint32_t)(i % n) == me) return;
     g1a q;
-    int32_t st = g1_decompress(shares + i * 48, q);
-    if (st == HBX_PT_OK && !g1_is_torsion_free(q)) st = HBX_PT_NOT_IN_SUBGROUP;
+    int32_t st = g1_decompress_d(shares + i * 48, q);
+    if (st == HBX_PT_OK && !g1_is_torsion_free_d(q)) st = HBX_PT_NOT_IN_SUBGROUP;
     S_status[i] = st;
     S[i] = q;
     return;
@@ -148,8 +149,8 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
     const uint32_t k = (bid - hash_blocks) * blockDim.x + threadIdx.x;
     if (k < p) {
       g1a u;
-      int32_t st = g1_decompress(u_comp + (size_t)k * 48, u);
-      if (st == HBX_PT_OK && !g1_is_torsion_free(u)) st = HBX_PT_NOT_IN_SUBGROUP;
+      int32_t st = g1_decompress_d(u_comp + (size_t)k * 48, u);
+      if (st == HBX_PT_OK && !g1_is_torsion_free_d(u)) st = HBX_PT_NOT_IN_SUBGROUP;
       dec_st[k] = st;
       U[k] = u;
     } else if (own_sk && k >= 2 * pw && k < 2 * pw + 2 * p) {
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
       const uint32_t h = k - 2 * pw, j = h >> 1;
       g1a u;
       g1j part = g1_identity();
-      if (g1_decompress(u_comp + (size_t)j * 48, u) == HBX_PT_OK) {
+      if (g1_decompress_d(u_comp + (size_t)j * 48, u) == HBX_PT_OK) {
         uint32_t k1[4], k2[4];
         g1_glv_split(own_sk, k1, k2);
         if (h & 1) u.x = fq_mul(u.x, fq_from_const(G1_BETA));
@@ -205,151 +206,15 @@ __global__ void __launch_bounds__(64) k_prepare_ct(const uint8_t* __restrict__ u
 // Lanes per G2 point in k_prepare_lines.
 constexpr int LINE_K = 16;
 
+
 #if HBX_IN_TU(1)
-// line_dbl_step (pairing.hpp) on the LINE_K lanes of a group that all hold T: its 26 Fq
-// products as three rounds of independent products, one per lane (10, 14 and 8 lanes busy),
-// exchanged by ds_bpermute; Fq2 products by schoolbook.  Same values mod p as line_dbl_step.
-__device__ __forceinline__ void line_dbl_step_group(g2j& T, fq2& c0, fq2& c1, fq2& c2, int gl, int gbase) {
-  const fq x0 = T.x.c0, x1 = T.x.c1, y0 = T.y.c0, y1 = T.y.c1, z0 = T.z.c0, z1 = T.z.c1;
-  // round 1: A = X^2 (0, 1), B = Y^2 (2, 3), ZZ = Z^2 (4, 5), Y Z (6..9)
-  fq r;
-  {
-    const fq a[16] = {fq_add(x0, x1), x0, fq_add(y0, y1), y0, fq_add(z0, z1), z0, y0, y1, y0, y1,
-                      x0, x0, x0, x0, x0, x0};
-    const fq b[16] = {fq_sub(x0, x1), x1, fq_sub(y0, y1), y1, fq_sub(z0, z1), z1, z0, z1, z1, z0,
-                      x1, x1, x1, x1, x1, x1};
-    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
-  }
-  const fq2 A = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
-  const fq2 B = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
-  const fq2 ZZ = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
-  const fq2 YZ = fq2{fq_sub(fq_from_row<6>(r), fq_from_row<7>(r)),
-                     fq_add(fq_from_row<8>(r), fq_from_row<9>(r))};
-  // round 2: C = B^2 (0, 1), (X + B)^2 (2, 3), F = E^2 (4, 5), E X (6..9), E ZZ (10..13)
-  const fq2 E = fq2_add(fq2_dbl(A), A);
-  const fq2 S = fq2_add(T.x, B);
-  {
-    const fq a[16] = {fq_add(B.c0, B.c1), B.c0, fq_add(S.c0, S.c1), S.c0, fq_add(E.c0, E.c1), E.c0,
-                      E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c0};
-    const fq b[16] = {fq_sub(B.c0, B.c1), B.c1, fq_sub(S.c0, S.c1), S.c1, fq_sub(E.c0, E.c1), E.c1,
-                      x0, x1, x1, x0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0, E.c1, E.c1};
-    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
-  }
-  const fq2 C = fq2{fq_from_row<0>(r), fq_dbl(fq_from_row<1>(r))};
-  const fq2 TT = fq2{fq_from_row<2>(r), fq_dbl(fq_from_row<3>(r))};
-  const fq2 F = fq2{fq_from_row<4>(r), fq_dbl(fq_from_row<5>(r))};
-  const fq2 EX = fq2{fq_sub(fq_from_row<6>(r), fq_from_row<7>(r)),
-                     fq_add(fq_from_row<8>(r), fq_from_row<9>(r))};
-  const fq2 EZZ = fq2{fq_sub(fq_from_row<10>(r), fq_from_row<11>(r)),
-                      fq_add(fq_from_row<12>(r), fq_from_row<13>(r))};
-  c0 = fq2_sub(EX, fq2_dbl(B));
-  c1 = fq2_neg(EZZ);
-  const fq2 D = fq2_dbl(fq2_sub(fq2_sub(TT, A), C));
-  const fq2 X3 = fq2_sub(F, fq2_dbl(D));
-  const fq2 Z3 = fq2_dbl(YZ);
-  // round 3: E (D - X3) (0..3), c2 = Z3 ZZ (4..7)
-  const fq2 G = fq2_sub(D, X3);
-  {
-    const fq a[16] = {E.c0, E.c1, E.c0, E.c1, Z3.c0, Z3.c1, Z3.c0, Z3.c1,
-                      E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0};
-    const fq b[16] = {G.c0, G.c1, G.c1, G.c0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0,
-                      G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0};
-    r = fq_mul_inl(fq_sel16(gl, a), fq_sel16(gl, b));
-  }
-  const fq2 EG = fq2{fq_sub(fq_from_row<0>(r), fq_from_row<1>(r)),
-                     fq_add(fq_from_row<2>(r), fq_from_row<3>(r))};
-  c2 = fq2{fq_sub(fq_from_row<4>(r), fq_from_row<5>(r)),
-           fq_add(fq_from_row<6>(r), fq_from_row<7>(r))};
-  const fq2 C8 = fq2_dbl(fq2_dbl(fq2_dbl(C)));
-  T = g2j{X3, fq2_sub(EG, C8), Z3};
-}
-
-// line_add_step (pairing.hpp) on the LINE_K lanes of a group that all hold T and Q: its Fq
-// products as five rounds of independent products, one per lane (hash.hpp round16), instead of
-// ~60 dependent products on every lane (57.6 us per step, profiles/r03l_microbench_lines.txt).
-// Same values as line_add_step: num = Y - yQ Z^3, den = Z (X - xQ Z^2), c0 = num xQ - yQ den,
-// c1 = -num, c2 = den; T <- T + Q (madd-2007-bl).
-__device__ __forceinline__ void line_add_step_group(g2j& T, const g2a& Q, fq2& c0, fq2& c1, fq2& c2, int gl) {
-  round16 R;
-  r16_clear(R);
-  // round 1: Z1Z1 = Z^2 (0, 1), yQ Z (2..5)
-  r16_sqr(R, 0, T.z);
-  r16_mul(R, 2, Q.y, T.z);
-  fq r = r16_run(R, gl);
-  const fq2 Z1Z1 = r16_get_sqr<0>(r), YqZ = r16_get_mul<2>(r);
-  // round 2: U2 = xQ Z1Z1 (0..3), S2 = yQ Z Z1Z1 (4..7)
-  r16_mul(R, 0, Q.x, Z1Z1);
-  r16_mul(R, 4, YqZ, Z1Z1);
-  r = r16_run(R, gl);
-  const fq2 U2 = r16_get_mul<0>(r), S2 = r16_get_mul<4>(r);
-  const fq2 H = fq2_sub(U2, T.x);  // -(X - xQ Z^2)
-  const fq2 num = fq2_sub(T.y, S2);
-  const fq2 rr = fq2_dbl(fq2_sub(S2, T.y));
-  // round 3: Z H (0..3), HH = H^2 (4, 5), num xQ (6..9), rr^2 (10, 11), (Z + H)^2 (12, 13)
-  r16_mul(R, 0, T.z, H);
-  r16_sqr(R, 4, H);
-  r16_mul(R, 6, num, Q.x);
-  r16_sqr(R, 10, rr);
-  r16_sqr(R, 12, fq2_add(T.z, H));
-  r = r16_run(R, gl);
-  const fq2 den = fq2_neg(r16_get_mul<0>(r));
-  const fq2 HH = r16_get_sqr<4>(r), NX = r16_get_mul<6>(r), RR = r16_get_sqr<10>(r), ZHs = r16_get_sqr<12>(r);
-  const fq2 I = fq2_dbl(fq2_dbl(HH));
-  c1 = fq2_neg(num);
-  c2 = den;
-  // round 4: yQ den (0..3), J = H I (4..7), V = X I (8..11)
-  r16_mul(R, 0, Q.y, den);
-  r16_mul(R, 4, H, I);
-  r16_mul(R, 8, T.x, I);
-  r = r16_run(R, gl);
-  const fq2 YD = r16_get_mul<0>(r), J = r16_get_mul<4>(r), V = r16_get_mul<8>(r);
-  c0 = fq2_sub(NX, YD);
-  const fq2 X3 = fq2_sub(fq2_sub(RR, J), fq2_dbl(V));
-  // round 5: rr (V - X3) (0..3), Y J (4..7)
-  r16_mul(R, 0, rr, fq2_sub(V, X3));
-  r16_mul(R, 4, T.y, J);
-  r = r16_run(R, gl);
-  const fq2 Y3 = fq2_sub(r16_get_mul<0>(r), fq2_dbl(r16_get_mul<4>(r)));
-  T = g2j{X3, Y3, fq2_sub(fq2_sub(ZHs, Z1Z1), HH)};
-}
-
-// g2_raw_lines on a lane group; group lane 0 writes the lines.  GADD: the addition steps as grouped
-// rounds (line_add_step_group) -- lower latency, but the kernel's register footprint grows and a
-// concurrent epoch's full-chip share checks then overlap it worse (two N = 256 epochs in flight:
-// 28.2 -> 32.5 ms per epoch), so only small launches use it (hbx_api.hip).
-template <bool GADD>
-__device__ void g2_raw_lines_group(const g2a& Q, line_pre* out, fq2* c2out, int gl, int gbase) {
-  g2j T = g2_from_affine(Q);
-  int k = 0;
-  for (int i = 62; i >= 0; i--) {
-    fq2 c0, c1, c2;
-    line_dbl_step_group(T, c0, c1, c2, gl, gbase);
-    if (gl == 0) {
-      out[k].c0 = c0;
-      out[k].c1 = c1;
-      c2out[k] = c2;
-    }
-    k++;
-    if ((BLS_X >> i) & 1) {
-      if (GADD) line_add_step_group(T, Q, c0, c1, c2, gl);
-      else line_add_step(T, Q, c0, c1, c2);
-      if (gl == 0) {
-        out[k].c0 = c0;
-        out[k].c1 = c1;
-        c2out[k] = c2;
-      }
-      k++;
-    }
-  }
-}
-
 // LINE_K lanes per G2 point: the 68 raw lines (c2 into `scratch`, count x 68 Fq2), normalised by
 // k_normalise_lines.  With `dec_st` (ciphertext points), the group of point 2j also
 // settles ct_ok[j]: U_j and W_j must decode (threshold_crypto deserialisation); otherwise H_j is
 // replaced by the identity and the proposer's checks are gated off.
 template <bool GADD>
 __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uint32_t count,
-                                                      line_pre* __restrict__ lines, fq2* __restrict__ scratch,
+                                                      line_pre_d* __restrict__ raw, fq2d* __restrict__ scratch,
                                                       const int32_t* __restrict__ dec_st, uint32_t p,
                                                       uint8_t* __restrict__ ct_ok, const g1j* __restrict__ own_part,
                                                       g1a* __restrict__ own_S, uint32_t n, uint32_t me,
@@ -398,40 +263,46 @@ __global__ void __launch_bounds__(64) k_prepare_lines(g2a* __restrict__ pts, uin
   }
   if (q.inf) {
     if (gl == 0) {
+      const fq2d one{fqd_const(FQD_ONE), fqd_zero()}, zero{fqd_zero(), fqd_zero()};
       for (int i = 0; i < MILLER_LINES; i++) {
-        lines[(size_t)k * MILLER_LINES + i].c0 = fq2_one();
-        lines[(size_t)k * MILLER_LINES + i].c1 = fq2_zero();
-        scratch[(size_t)k * MILLER_LINES + i] = fq2_one();
+        raw[(size_t)k * MILLER_LINES + i] = line_pre_d{one, zero};
+        scratch[(size_t)k * MILLER_LINES + i] = one;
       }
     }
     return;
   }
-  g2_raw_lines_group<GADD>(q, lines + (size_t)k * MILLER_LINES, scratch + (size_t)k * MILLER_LINES, gl, gbase);
+  // the steps in the digit tower on the group (groupd.hpp); raw lines in digit form
+  (void)gbase;
+  g2d_raw_lines_group<GADD>(fq2d_from_fq2(q.x), fq2d_from_fq2(q.y), raw + (size_t)k * MILLER_LINES,
+                            scratch + (size_t)k * MILLER_LINES, gl);
 }
-template __global__ void k_prepare_lines<true>(g2a*, uint32_t, line_pre*, fq2*, const int32_t*, uint32_t, uint8_t*,
+template __global__ void k_prepare_lines<true>(g2a*, uint32_t, line_pre_d*, fq2d*, const int32_t*, uint32_t, uint8_t*,
                                                const g1j*, g1a*, uint32_t, uint32_t, g1a*, int32_t*, const g2j*);
-template __global__ void k_prepare_lines<false>(g2a*, uint32_t, line_pre*, fq2*, const int32_t*, uint32_t, uint8_t*,
+template __global__ void k_prepare_lines<false>(g2a*, uint32_t, line_pre_d*, fq2d*, const int32_t*, uint32_t, uint8_t*,
                                                 const g1j*, g1a*, uint32_t, uint32_t, g1a*, int32_t*, const g2j*);
 
 // Second half of the line preparation: one lane per raw line, (c0, c1) /= c2.  68 independent
 // Fq2 inversions replace the batched inversion (3 x 68 Fq2 products plus one inversion) that
 // used to sit at the end of each point's sequential chain: the chain of k_prepare_lines is the
 // 68 T steps only, and this launch is 68x wider and one inversion deep.
+// The raw lines come in digit form (k_prepare_lines: (c0, c1) in lines_d, c2 in `c2`); the
+// normalised lines go out in both forms, lines_d overwritten in place.
 __global__ void __launch_bounds__(64) k_normalise_lines(line_pre* __restrict__ lines,
-                                                        const fq2* __restrict__ c2, uint32_t count,
+                                                        const fq2d* __restrict__ c2, uint32_t count,
                                                         line_pre_d* __restrict__ lines_d,
                                                         const g2a* __restrict__ pts, const g2j* __restrict__ Hj) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
-  line_pre l = lines[k];
+  const line_pre_d rd = lines_d[k];
+  line_pre l{fq2d_to_fq2(rd.c0), fq2d_to_fq2(rd.c1)};
   const uint32_t pt = k / MILLER_LINES;
   // lines of a Jacobian hash point (k_prepare_lines with Hj) unless it was replaced by the
   // identity; z = 1 otherwise (one code path for the wave: a branch would run both inversions)
   fq2 z = fq2_one();
   if (Hj && (pt & 1) == 0 && !pts[pt].inf) z = Hj[pt >> 1].z;
-  g2_normalise_line_z(l, c2[k], z);
+  g2_normalise_line_z(l, fq2d_to_fq2(c2[k]), z);
   lines[k] = l;
-  if (lines_d) lines_d[k] = line_to_d(l);
+  lines_d[k] = line_to_d(l);
 }
 #endif
 
@@ -1381,8 +1252,8 @@ __global__ void __launch_bounds__(256) k_decompress_shares(const uint8_t* __rest
     return;
   }
   g1a p;
-  int32_t st = g1_decompress(shares + i * 48, p);
-  if (st == HBX_PT_OK && !g1_is_torsion_free(p)) st = HBX_PT_NOT_IN_SUBGROUP;
+  int32_t st = g1_decompress_d(shares + i * 48, p);
+  if (st == HBX_PT_OK && !g1_is_torsion_free_d(p)) st = HBX_PT_NOT_IN_SUBGROUP;
   status[i] = st;
   S[i] = p;
 }
@@ -1595,8 +1466,8 @@ __global__ void __launch_bounds__(64) k_verify_sigs(const uint8_t* __restrict__ 
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   g1a pk;
-  int32_t st = g1_decompress(pk48 + (size_t)i * 48, pk);
-  if (st == HBX_PT_OK && !g1_is_torsion_free(pk)) st = HBX_PT_NOT_IN_SUBGROUP;
+  int32_t st = g1_decompress_d(pk48 + (size_t)i * 48, pk);
+  if (st == HBX_PT_OK && !g1_is_torsion_free_d(pk)) st = HBX_PT_NOT_IN_SUBGROUP;
   const bool pk_ok = st == HBX_PT_OK || st == HBX_PT_INFINITY;
   const bool sig_ok = sig_st[i] == HBX_PT_OK || sig_st[i] == HBX_PT_INFINITY;
   if (!pk_ok || !sig_ok) {

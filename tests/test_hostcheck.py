@@ -444,10 +444,20 @@ def test_subgroup_checks_match_order_r(hc):
         q = _rand_curve_point_g2(rnd)
         in_g2 = bls.g2_mul(q, bls.R) is None
         assert hc.hc_g2_torsion_free(_be(q[0][1]) + _be(q[0][0]) + _be(q[1][1]) + _be(q[1][0])) == int(in_g2)
-    # a point of small order times a G1 point: on the curve, not in G1
-    small = bls.g1_mul(_rand_curve_point_g1(rnd), bls.R)  # order divides h1
-    mixed = bls.g1_add(small, bls.g1_mul(bls.G1_GEN, 9))
-    assert hc.hc_g1_torsion_free(_be(mixed[0]), _be(mixed[1])) == 0
+    # a point of small order times a G1 point: on the curve, not in G1 (and the small-order points
+    # themselves: their double-and-add meets the identity and +-P, the exact special cases)
+    for _ in range(3):
+        small = bls.g1_mul(_rand_curve_point_g1(rnd), bls.R)  # order divides h1
+        if small is None:
+            continue
+        assert hc.hc_g1_torsion_free(_be(small[0]), _be(small[1])) == 0
+        mixed = bls.g1_add(small, bls.g1_mul(bls.G1_GEN, 9))
+        assert hc.hc_g1_torsion_free(_be(mixed[0]), _be(mixed[1])) == 0
+    for k in (3, 11, 10177):  # points of order k | h1 (k prime): [h1 / k] of a random point
+        h1 = 0x396C8C005555E1568C00AAAB0000AAAB
+        q = bls.g1_mul(_rand_curve_point_g1(rnd), bls.R * (h1 // k))
+        if q is not None:
+            assert hc.hc_g1_torsion_free(_be(q[0]), _be(q[1])) == 0
 
 
 def test_g2_membership_from_miller_T(hc):

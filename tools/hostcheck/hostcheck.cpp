@@ -6,6 +6,7 @@
 #include "../../hbbft_amd/csrc/pairingd.hpp"
 #include "../../hbbft_amd/csrc/fe1d.hpp"
 #include "../../hbbft_amd/csrc/g2d.hpp"
+#include "../../hbbft_amd/csrc/g1d.hpp"
 #include "../../hbbft_amd/csrc/hash.hpp"
 using namespace hbx;
 extern "C" {
@@ -37,7 +38,9 @@ int hc_g1_torsion_free(const uint8_t* x48, const uint8_t* y48) {
   p.inf = false;
   const fq rhs = fq_add(fq_mul(fq_sqr(p.x), p.x), fq_from_const(FQ_B1));
   if (!fq_eq(fq_sqr(p.y), rhs)) return -1;
-  return g1_is_torsion_free(p) ? 1 : 0;
+  // the 12-limb check and the digit-tower one (g1d.hpp, the decode kernels'): -2 if they differ
+  const bool a = g1_is_torsion_free(p), b = g1_is_torsion_free_d(p);
+  return a != b ? -2 : a ? 1 : 0;
 }
 int hc_g2_torsion_free(const uint8_t* xy192) {
   g2a q;
@@ -67,6 +70,9 @@ void hc_fr_inv_raw(const uint32_t* a, uint32_t* out) {
 }
 int hc_g1_roundtrip(const uint8_t* in48, uint8_t* out48) {
   g1a p; int st = g1_decompress(in48, p);
+  // the decode kernels' digit-tower square root gives the same status and point (-100 if not)
+  g1a q; const int sd = g1_decompress_d(in48, q);
+  if (sd != st || (st == HBX_PT_OK && !(fq_eq(p.x, q.x) && fq_eq(p.y, q.y)))) return -100;
   if (st != HBX_PT_OK && st != HBX_PT_INFINITY) return st;
   g1_compress(p, out48); return st;
 }
