@@ -24,14 +24,22 @@
 namespace hbx {
 #if defined(__HIPCC__)
 
-// lane K of the calling lane's 16-lane row, to every lane of the row (DPP row_newbcast per digit)
+// lane K of the calling lane's 16-lane row, to every lane of the row (DPP row_newbcast per digit).
+// Each moved digit is pinned in a register (HBX_LAUNDER) so the compiler cannot fold the move into
+// its consumer as a DPP-modified add / subtract: in the fqd_pick addition such folded row_newbcast
+// operations produced wrong sums on gfx950 (tools/microbench/addcmp.hip: Y1 Z2 differed from the
+// same expression outside the function; with the moves pinned both agree and the hash-to-G2
+// checksum of profiles/r05o_hashg2.txt is reproduced).
 template <int K>
 __device__ __forceinline__ fqd fqd_from_row(const fqd& v) {
   static_assert(K >= 0 && K < 16, "row lane");
   dpp_guard_src<16, K>();
   fqd r;
 #pragma unroll
-  for (int i = 0; i < 14; i++) r.d[i] = __builtin_amdgcn_update_dpp(0, v.d[i], 0x150 + K, 0xf, 0xf, false);
+  for (int i = 0; i < 14; i++) {
+    r.d[i] = __builtin_amdgcn_update_dpp(0, v.d[i], 0x150 + K, 0xf, 0xf, false);
+    HBX_LAUNDER(r.d[i]);
+  }
   return r;
 }
 __device__ __forceinline__ fqd fqd_sel8(int s, const fqd& v0, const fqd& v1, const fqd& v2, const fqd& v3, const fqd& v4,
@@ -45,17 +53,27 @@ __device__ __forceinline__ fqd fqd_sel8(int s, const fqd& v0, const fqd& v1, con
   }
   return r;
 }
-__device__ __forceinline__ fqd fqd_sel16(int s, const fqd (&v)[16]) {
+// a lane's operand among 16 candidates given as separate values (a 16-entry candidate array --
+// two per round -- was kept in scratch memory: 1,093 scratch accesses per addition)
+__device__ __forceinline__ int32_t pick_digit(int, int, int, int32_t t) { return t; }
+template <class... R>
+__device__ __forceinline__ int32_t pick_digit(int s, int i, int k, int32_t t, const fqd& v, const R&... rest) {
+  return pick_digit(s, i, k + 1, s == k ? v.d[i] : t, rest...);
+}
+template <class... R>
+__device__ __forceinline__ fqd fqd_pick(int s, const fqd& v0, const R&... rest) {
+  static_assert(sizeof...(R) == 15, "16 candidates");
   fqd r;
 #pragma unroll
-  for (int i = 0; i < 14; i++) {
-    int32_t t = v[0].d[i];
-#pragma unroll
-    for (int k = 1; k < 16; k++) t = (s == k) ? v[k].d[i] : t;
-    r.d[i] = t;
-  }
+  for (int i = 0; i < 14; i++) r.d[i] = pick_digit(s, i, 1, v0.d[i], rest...);
   return r;
 }
+// candidate lists of one Fq2 product (4 lanes, schoolbook) or square (2 lanes)
+#define GD_MULA(x) (x).c0, (x).c1, (x).c0, (x).c1
+#define GD_MULB(y) (y).c0, (y).c1, (y).c1, (y).c0
+#define GD_SQRA(x) fqd_add((x).c0, (x).c1), (x).c0
+#define GD_SQRB(x) fqd_sub((x).c0, (x).c1), (x).c1
+
 // Fq2 results of a round: a square from rows (K, K + 1) = ((a0 + a1)(a0 - a1), a0 a1), a product
 // from rows (K .. K + 3) = (a0 b0, a1 b1, a0 b1, a1 b0) (schoolbook).  Digits below 2^29.
 template <int K>
@@ -94,82 +112,59 @@ __device__ __forceinline__ g2jd g2d_dbl_n_group(g2jd p, int n, int gl) {
   return p;
 }
 
-// a round of up to 16 independent Fq products, one per lane of a 16-lane group
-struct round16d {
-  fqd a[16], b[16];
-};
-__device__ __forceinline__ void r16d_mul(round16d& R, int k, const fq2d& x, const fq2d& y) {
-  R.a[k] = x.c0; R.b[k] = y.c0;
-  R.a[k + 1] = x.c1; R.b[k + 1] = y.c1;
-  R.a[k + 2] = x.c0; R.b[k + 2] = y.c1;
-  R.a[k + 3] = x.c1; R.b[k + 3] = y.c0;
-}
-__device__ __forceinline__ void r16d_sqr(round16d& R, int k, const fq2d& x) {
-  R.a[k] = fqd_add(x.c0, x.c1); R.b[k] = fqd_sub(x.c0, x.c1);
-  R.a[k + 1] = x.c0; R.b[k + 1] = x.c1;
-}
-__device__ __forceinline__ void r16d_clear(round16d& R) {
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    R.a[i] = fqd_zero();
-    R.b[i] = fqd_zero();
-  }
-}
-__device__ __forceinline__ fqd r16d_run(const round16d& R, int gl) { return fqd_mul(fqd_sel16(gl, R.a), fqd_sel16(gl, R.b)); }
-
 // P + Q on the 16 lanes of a group (hash.hpp g2_add_group, add-2007-bl) in five rounds, the same
 // special cases as g2_add by exact tests.  Relaxed in and out.
-__device__ __noinline__ g2jd g2d_add_group(const g2jd& p, const g2jd& q, int gl) {
+__device__ __forceinline__ g2jd g2d_add_group_i(const g2jd& p, const g2jd& q, int gl) {
   if (fq2d_is_zero_mod(p.z)) return q;
   if (fq2d_is_zero_mod(q.z)) return p;
-  round16d R;
-  r16d_clear(R);
-  // round 1: Z1^2, Z2^2, Y1 Z2, Y2 Z1, (Z1 + Z2)^2
-  r16d_sqr(R, 0, p.z);
-  r16d_sqr(R, 2, q.z);
-  r16d_mul(R, 4, p.y, q.z);
-  r16d_mul(R, 8, q.y, p.z);
-  r16d_sqr(R, 12, fq2d_relax(fq2d_add(p.z, q.z)));
-  fqd r = r16d_run(R, gl);
+  const fqd z = fqd_zero();
+  // round 1: Z1^2 (0, 1), Z2^2 (2, 3), Y1 Z2 (4..7), Y2 Z1 (8..11), (Z1 + Z2)^2 (12, 13)
+  fqd r;
+  {
+    const fq2d zs = fq2d_relax(fq2d_add(p.z, q.z));
+    r = fqd_mul(fqd_pick(gl, GD_SQRA(p.z), GD_SQRA(q.z), GD_MULA(p.y), GD_MULA(q.y), GD_SQRA(zs), z, z),
+                fqd_pick(gl, GD_SQRB(p.z), GD_SQRB(q.z), GD_MULB(q.z), GD_MULB(p.z), GD_SQRB(zs), z, z));
+  }
   const fq2d Z1Z1 = rows_sqr<0>(r), Z2Z2 = rows_sqr<2>(r);
   const fq2d Y1Z2 = rows_mul<4>(r), Y2Z1 = rows_mul<8>(r);
   const fq2d ZS = rows_sqr<12>(r);
-  // round 2: U1, U2, S1, S2
-  r16d_mul(R, 0, p.x, Z2Z2);
-  r16d_mul(R, 4, q.x, Z1Z1);
-  r16d_mul(R, 8, Y1Z2, Z2Z2);
-  r16d_mul(R, 12, Y2Z1, Z1Z1);
-  r = r16d_run(R, gl);
-  const fq2d U1 = rows_mul<0>(r), U2 = rows_mul<4>(r);
-  const fq2d S1 = rows_mul<8>(r), S2 = rows_mul<12>(r);
-  const fq2d H = fq2d_relax(fq2d_sub(U2, U1));
-  const fq2d dS = fq2d_relax(fq2d_sub(S2, S1));
+  // round 2: U1 (0..3), U2 (4..7), S1 (8..11), S2 (12..15)
+  r = fqd_mul(fqd_pick(gl, GD_MULA(p.x), GD_MULA(q.x), GD_MULA(Y1Z2), GD_MULA(Y2Z1)),
+              fqd_pick(gl, GD_MULB(Z2Z2), GD_MULB(Z1Z1), GD_MULB(Z2Z2), GD_MULB(Z1Z1)));
+  const fq2d U1 = rows_mul<0>(r), S1 = rows_mul<8>(r);
+  const fq2d H = fq2d_relax(fq2d_sub(rows_mul<4>(r), U1));
+  const fq2d dS = fq2d_relax(fq2d_sub(rows_mul<12>(r), S1));
   if (fq2d_is_zero_mod(H)) {
     if (fq2d_is_zero_mod(dS)) return g2d_dbl_group(p, gl);
     return g2d_identity();
   }
   const fq2d rr = fq2d_dbl(dS);
-  // round 3: I = (2H)^2 = 4 H^2, r^2 = 4 dS^2, Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
-  r16d_sqr(R, 0, H);
-  r16d_sqr(R, 2, dS);
-  r16d_mul(R, 4, fq2d_relax(fq2d_sub(fq2d_sub(ZS, Z1Z1), Z2Z2)), H);
-  r = r16d_run(R, gl);
-  const fq2d I = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<0>(r))));
-  const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<2>(r))));
+  // round 3: H^2 (0, 1), dS^2 (2, 3), ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H (4..7)
+  {
+    const fq2d zz = fq2d_relax(fq2d_sub(fq2d_sub(ZS, Z1Z1), Z2Z2));
+    r = fqd_mul(fqd_pick(gl, GD_SQRA(H), GD_SQRA(dS), GD_MULA(zz), z, z, z, z, z, z, z, z),
+                fqd_pick(gl, GD_SQRB(H), GD_SQRB(dS), GD_MULB(H), z, z, z, z, z, z, z, z));
+  }
+  const fq2d I = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<0>(r))));   // (2H)^2
+  const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<2>(r))));  // rr^2
   const fq2d Z3 = fq2d_relax(rows_mul<4>(r));
-  // round 4: J = H I, V = U1 I
-  r16d_mul(R, 0, H, I);
-  r16d_mul(R, 4, U1, I);
-  r = r16d_run(R, gl);
+  // round 4: J = H I (0..3), V = U1 I (4..7)
+  r = fqd_mul(fqd_pick(gl, GD_MULA(H), GD_MULA(U1), z, z, z, z, z, z, z, z),
+              fqd_pick(gl, GD_MULB(I), GD_MULB(I), z, z, z, z, z, z, z, z));
   const fq2d J = rows_mul<0>(r), V = rows_mul<4>(r);
   const fq2d X3 = fq2d_relax(fq2d_sub(fq2d_relax(fq2d_sub(RR, J)), fq2d_dbl(V)));
-  // round 5: r (V - X3), S1 J
-  r16d_mul(R, 0, rr, fq2d_sub(V, X3));
-  r16d_mul(R, 4, S1, J);
-  r = r16d_run(R, gl);
+  // round 5: rr (V - X3) (0..3), S1 J (4..7)
+  {
+    const fq2d w = fq2d_sub(V, X3);
+    r = fqd_mul(fqd_pick(gl, GD_MULA(rr), GD_MULA(S1), z, z, z, z, z, z, z, z),
+                fqd_pick(gl, GD_MULB(w), GD_MULB(J), z, z, z, z, z, z, z, z));
+  }
   const fq2d Y3 = fq2d_relax(fq2d_sub(rows_mul<0>(r), fq2d_dbl(rows_mul<4>(r))));
   return g2jd{X3, Y3, Z3};
 }
+// one out-of-line copy for the clearing's few combining additions; the multiplication loop inlines
+// its own (a call there saved and restored the caller's live point around every addition)
+__device__ __noinline__ g2jd g2d_add_group(const g2jd& p, const g2jd& q, int gl) { return g2d_add_group_i(p, q, gl); }
 __device__ __forceinline__ g2jd g2d_neg(const g2jd& p) { return g2jd{p.x, fq2d_neg(p.y), p.z}; }
 __device__ __forceinline__ g2jd g2d_sub_group(const g2jd& p, const g2jd& q, int gl) { return g2d_add_group(p, g2d_neg(q), gl); }
 
@@ -186,7 +181,7 @@ __device__ __noinline__ g2jd g2d_mul_u64_group(const g2jd& p, uint64_t k, int gl
   const int top = 63 - __builtin_clzll(k);
   for (int i = top - 1; i >= 0; i--) {
     acc = g2d_dbl_group(acc, gl);
-    if ((k >> i) & 1) acc = g2d_add_group(acc, p, gl);
+    if ((k >> i) & 1) acc = g2d_add_group_i(acc, p, gl);
   }
   return acc;
 }
@@ -230,24 +225,14 @@ __device__ __noinline__ g2jd g2d_clear_cofactor_group(const g2jd& P, int gl, boo
 // Relaxed in and out (T and the line's coefficients).
 __device__ __forceinline__ void line_dbl_step_groupd(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2, int gl) {
   const fqd x0 = T.x.c0, x1 = T.x.c1, y0 = T.y.c0, y1 = T.y.c1, z0 = T.z.c0, z1 = T.z.c1;
-  fqd r;
-  {
-    const fqd a[16] = {fqd_add(x0, x1), x0, fqd_add(y0, y1), y0, fqd_add(z0, z1), z0, y0, y1, y0, y1,
-                       x0, x0, x0, x0, x0, x0};
-    const fqd b[16] = {fqd_sub(x0, x1), x1, fqd_sub(y0, y1), y1, fqd_sub(z0, z1), z1, z0, z1, z1, z0,
-                       x1, x1, x1, x1, x1, x1};
-    r = fqd_mul(fqd_sel16(gl, a), fqd_sel16(gl, b));
-  }
+  const fqd z = fqd_zero();
+  fqd r = fqd_mul(fqd_pick(gl, GD_SQRA(T.x), GD_SQRA(T.y), GD_SQRA(T.z), GD_MULA(T.y), z, z, z, z, z, z),
+                  fqd_pick(gl, GD_SQRB(T.x), GD_SQRB(T.y), GD_SQRB(T.z), GD_MULB(T.z), z, z, z, z, z, z));
   const fq2d A = rows_sqr<0>(r), B = rows_sqr<2>(r), ZZ = rows_sqr<4>(r), YZ = rows_mul<6>(r);
   const fq2d E = fq2d_relax(fq2d_add(fq2d_dbl(A), A));
   const fq2d S = fq2d_relax(fq2d_add(T.x, B));
-  {
-    const fqd a[16] = {fqd_add(B.c0, B.c1), B.c0, fqd_add(S.c0, S.c1), S.c0, fqd_add(E.c0, E.c1), E.c0,
-                       E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c1, E.c0, E.c0};
-    const fqd b[16] = {fqd_sub(B.c0, B.c1), B.c1, fqd_sub(S.c0, S.c1), S.c1, fqd_sub(E.c0, E.c1), E.c1,
-                       x0, x1, x1, x0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0, E.c1, E.c1};
-    r = fqd_mul(fqd_sel16(gl, a), fqd_sel16(gl, b));
-  }
+  r = fqd_mul(fqd_pick(gl, GD_SQRA(B), GD_SQRA(S), GD_SQRA(E), GD_MULA(E), GD_MULA(E), z, z),
+              fqd_pick(gl, GD_SQRB(B), GD_SQRB(S), GD_SQRB(E), GD_MULB(T.x), GD_MULB(ZZ), z, z));
   const fq2d C = rows_sqr<0>(r), TT = rows_sqr<2>(r), F = rows_sqr<4>(r), EX = rows_mul<6>(r), EZZ = rows_mul<10>(r);
   c0 = fq2d_relax(fq2d_sub(EX, fq2d_dbl(B)));
   c1 = fq2d_relax(fq2d_neg(EZZ));
@@ -255,11 +240,8 @@ __device__ __forceinline__ void line_dbl_step_groupd(g2jd& T, fq2d& c0, fq2d& c1
   const fq2d X3 = fq2d_relax(fq2d_sub(F, fq2d_dbl(D)));
   const fq2d Z3 = fq2d_relax(fq2d_dbl(YZ));
   const fq2d G = fq2d_sub(D, X3);
-  {
-    const fqd a[16] = {E.c0, E.c1, E.c0, E.c1, Z3.c0, Z3.c1, Z3.c0, Z3.c1, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0, E.c0};
-    const fqd b[16] = {G.c0, G.c1, G.c1, G.c0, ZZ.c0, ZZ.c1, ZZ.c1, ZZ.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0, G.c0};
-    r = fqd_mul(fqd_sel16(gl, a), fqd_sel16(gl, b));
-  }
+  r = fqd_mul(fqd_pick(gl, GD_MULA(E), GD_MULA(Z3), z, z, z, z, z, z, z, z),
+              fqd_pick(gl, GD_MULB(G), GD_MULB(ZZ), z, z, z, z, z, z, z, z));
   const fq2d EG = rows_mul<0>(r);
   c2 = fq2d_relax(rows_mul<4>(r));
   const fq2d C8 = fq2d_dbl(fq2d_dbl(fq2d_relax(fq2d_dbl(C))));
@@ -271,45 +253,39 @@ __device__ __forceinline__ void line_dbl_step_groupd(g2jd& T, fq2d& c0, fq2d& c1
 // the 16 lanes of a group in five rounds.  T relaxed in and out; (qx, qy) normalised.
 __device__ __forceinline__ void line_add_step_groupd(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1,
                                                      fq2d& c2, int gl) {
-  round16d R;
-  r16d_clear(R);
+  const fqd z = fqd_zero();
   // round 1: Z1Z1 = Z^2 (0, 1), yQ Z (2..5)
-  r16d_sqr(R, 0, T.z);
-  r16d_mul(R, 2, qy, T.z);
-  fqd r = r16d_run(R, gl);
+  fqd r = fqd_mul(fqd_pick(gl, GD_SQRA(T.z), GD_MULA(qy), z, z, z, z, z, z, z, z, z, z),
+                  fqd_pick(gl, GD_SQRB(T.z), GD_MULB(T.z), z, z, z, z, z, z, z, z, z, z));
   const fq2d Z1Z1 = rows_sqr<0>(r), YqZ = rows_mul<2>(r);
   // round 2: U2 = xQ Z1Z1 (0..3), S2 = yQ Z Z1Z1 (4..7)
-  r16d_mul(R, 0, qx, Z1Z1);
-  r16d_mul(R, 4, YqZ, Z1Z1);
-  r = r16d_run(R, gl);
-  const fq2d U2 = rows_mul<0>(r), S2 = rows_mul<4>(r);
-  const fq2d H = fq2d_relax(fq2d_sub(U2, T.x));  // -(X - xQ Z^2)
-  const fq2d num = fq2d_relax(fq2d_sub(T.y, S2));
-  // round 3: Z H (0..3), HH = H^2 (4, 5), num xQ (6..9), num^2 (10, 11), (Z + H)^2 (12, 13)
-  r16d_mul(R, 0, T.z, H);
-  r16d_sqr(R, 4, H);
-  r16d_mul(R, 6, num, qx);
-  r16d_sqr(R, 10, num);
-  r16d_sqr(R, 12, fq2d_relax(fq2d_add(T.z, H)));
-  r = r16d_run(R, gl);
-  const fq2d den = fq2d_relax(fq2d_neg(rows_mul<0>(r)));
+  r = fqd_mul(fqd_pick(gl, GD_MULA(qx), GD_MULA(YqZ), z, z, z, z, z, z, z, z),
+              fqd_pick(gl, GD_MULB(Z1Z1), GD_MULB(Z1Z1), z, z, z, z, z, z, z, z));
+  const fq2d H = fq2d_relax(fq2d_sub(rows_mul<0>(r), T.x));  // -(X - xQ Z^2)
+  const fq2d num = fq2d_relax(fq2d_sub(T.y, rows_mul<4>(r)));
+  // round 3: Z H (0..3), H^2 (4, 5), num xQ (6..9), num^2 (10, 11), (Z + H)^2 (12, 13)
+  {
+    const fq2d zh = fq2d_relax(fq2d_add(T.z, H));
+    r = fqd_mul(fqd_pick(gl, GD_MULA(T.z), GD_SQRA(H), GD_MULA(num), GD_SQRA(num), GD_SQRA(zh), z, z),
+                fqd_pick(gl, GD_MULB(H), GD_SQRB(H), GD_MULB(qx), GD_SQRB(num), GD_SQRB(zh), z, z));
+  }
+  c2 = fq2d_relax(fq2d_neg(rows_mul<0>(r)));  // den
   const fq2d HH = rows_sqr<4>(r), NX = rows_mul<6>(r), ZHs = rows_sqr<12>(r);
   const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<10>(r))));  // rr^2 = 4 num^2
   const fq2d I = fq2d_dbl(fq2d_relax(fq2d_dbl(HH)));
   c1 = fq2d_relax(fq2d_neg(num));
-  c2 = den;
   // round 4: yQ den (0..3), J = H I (4..7), V = X I (8..11)
-  r16d_mul(R, 0, qy, den);
-  r16d_mul(R, 4, H, I);
-  r16d_mul(R, 8, T.x, I);
-  r = r16d_run(R, gl);
-  const fq2d YD = rows_mul<0>(r), J = rows_mul<4>(r), V = rows_mul<8>(r);
-  c0 = fq2d_relax(fq2d_sub(NX, YD));
+  r = fqd_mul(fqd_pick(gl, GD_MULA(qy), GD_MULA(H), GD_MULA(T.x), z, z, z, z),
+              fqd_pick(gl, GD_MULB(c2), GD_MULB(I), GD_MULB(I), z, z, z, z));
+  c0 = fq2d_relax(fq2d_sub(NX, rows_mul<0>(r)));
+  const fq2d J = rows_mul<4>(r), V = rows_mul<8>(r);
   const fq2d X3 = fq2d_relax(fq2d_sub(fq2d_relax(fq2d_sub(RR, J)), fq2d_dbl(V)));
   // round 5: rr (V - X3) with rr = 2 (S2 - Y) = -2 num (0..3), Y J (4..7)
-  r16d_mul(R, 0, fq2d_dbl(c1), fq2d_sub(V, X3));
-  r16d_mul(R, 4, T.y, J);
-  r = r16d_run(R, gl);
+  {
+    const fq2d rr = fq2d_dbl(c1), w = fq2d_sub(V, X3);
+    r = fqd_mul(fqd_pick(gl, GD_MULA(rr), GD_MULA(T.y), z, z, z, z, z, z, z, z),
+                fqd_pick(gl, GD_MULB(w), GD_MULB(J), z, z, z, z, z, z, z, z));
+  }
   const fq2d Y3 = fq2d_relax(fq2d_sub(rows_mul<0>(r), fq2d_dbl(rows_mul<4>(r))));
   T = g2jd{X3, Y3, fq2d_relax(fq2d_sub(fq2d_sub(ZHs, Z1Z1), HH))};
 }
@@ -333,7 +309,7 @@ __device__ void g2d_raw_lines_group(const fq2d& qx, const fq2d& qy, line_pre_d* 
     k++;
     if ((BLS_X >> i) & 1) {
       if (GADD) line_add_step_groupd(T, qx, qy, c0, c1, c2, gl);
-      else line_add_step_d(T, qx, qy, c0, c1, c2);
+      else line_add_step_call(T, qx, qy, c0, c1, c2);
       if (gl == 0) {
         raw[k] = line_pre_d{c0, c1};
         c2out[k] = c2;

@@ -580,7 +580,8 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
   bool tf = true;
   if (res == HBX_SHARE_VALID) {
     // lane 0: e(pk_i, H'); lane 1: e(-[m] g1, sigma_i)  (H' = [m] H: the same verdict)
-    g2a Q = l1 ? sig[idx] : H[inst];
+    const g2a* qp = l1 ? sig + idx : H + inst;
+    const g2a Q = *qp;
     g1a P;
     if (l1) {
       P.x = fq_from_const(G1_MGEN_X);
@@ -590,26 +591,15 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
       P = pk[i];
     }
     const bool use = !(Q.inf || P.inf);  // a pairing with the identity contributes 1
-    g2jd T{};
-    const fq12d f = use ? miller_loop_gen_parked_d(fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), fqd_from_fq(P.x),
-                                                   fqd_from_fq(P.y), (lds_u32*)region + lane, T)
-                        : fq12d_one();
-    // sigma's membership in G2 from lane 1's T = [|x|] sigma (decode skipped it); lane 0's is H's
-    tf = !l1 || g2_torsion_free_from_T(T, Q);
     lds_u32* reg = (lds_u32*)region;
     const int pl = lane & ~1;
-    const slot2<lds_u32*> A{reg + pl, 64u}, B{reg + LDS_FQ6D_PACKED * 64 + pl, 64u};
-    // each lane parks its whole Fq12 in its slot (A: f_A, B: f_B), both halves
-    const slot2<lds_u32*>& mine = l1 ? B : A;
-    slot_put_fq6d(mine.half(0), mine.stride, fq6d_reduce(f.c0));
-    slot_put_fq6d(mine.half(1), mine.stride, fq6d_reduce(f.c1));
-    HBX_SEQ();
-    op_mul(B, A, false, false, l1);  // B = f_B f_A, lane k its half
-    HBX_SEQ();
+    g2jd T;
+    const fq6d f = miller_gen2d(qp, fqd_from_fq(P.x), fqd_from_fq(P.y), use, l1, (lds2)(reg + lane), reg + pl, T);
+    // sigma's membership in G2 from lane 1's T = [|x|] sigma (decode skipped it); lane 0's is H's
+    tf = !l1 || g2_torsion_free_from_T(T, Q);
+    // this lane's half of f_A f_B to the pair's global slot
     uint32_t* gb = gslot + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (2 * LDS_FQ6D_PACKED * 64) + pl;
-    const int h = l1 ? 1 : 0;
-#pragma unroll 6
-    for (int k = 0; k < LDS_FQ6D_PACKED; k++) gb[h + k * 64] = B.half(h)[k * 64];
+    slot_put_fq6d(gb + (l1 ? 1 : 0), 64u, fq6d_reduce(f));
   }
   // lane 1's membership bit to lane 0 (the pair is active or inactive together).  The exchange runs
   // on every lane before the bits are combined: inside `tf && ...` lane 1 (tf false) would skip it

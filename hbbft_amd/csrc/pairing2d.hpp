@@ -176,19 +176,23 @@ __device__ __forceinline__ void fq6d_mul_acc(fq6d& acc, const fq6d& a, Y y) {
 constexpr int ML_Y = 0, ML_C0 = 84, ML_C1 = 112;
 
 // (A0 + A1 w)^2 = (t - ab - v ab) + 2 ab w, ab = A0 A1, t = (A0 + A1)(A0 + v A1).  Reduced output.
+// Y2REG: Y's third coefficient stays in registers (words ML_Y .. ML_Y + 55 only).
+template <bool Y2REG = false>
 __device__ __forceinline__ fq6d sqr2d(const fq6d& A, bool l1, lds2 lds) {
   fq6d X;
+  fq2d y2;
   {
     const fq6d B = xchg_t(A);
     X = sel_t(l1, fq6d_norm(fq6d_add(A, B)), A);
     const fq6d Y = sel_t(l1, fq6d_norm(fq6d_add(B, fq6d_mul_v(A))), B);
     lds_put_fq2d_raw(lds, ML_Y, Y.c0);
     lds_put_fq2d_raw(lds, ML_Y + 28, Y.c1);
-    lds_put_fq2d_raw(lds, ML_Y + 56, Y.c2);
+    if (Y2REG) y2 = Y.c2;
+    else lds_put_fq2d_raw(lds, ML_Y + 56, Y.c2);
   }
   HBX_SEQ();
   fq6d P = fq6d_zero();  // lane 0: ab, lane 1: t
-  fq6d_mul_acc(P, X, [&](int q) { return lds_get_fq2d_raw(lds, ML_Y + 28 * q); });
+  fq6d_mul_acc(P, X, [&](int q) { return Y2REG && q == 2 ? y2 : lds_get_fq2d_raw(lds, ML_Y + 28 * q); });
   const fq6d Q = xchg_t(P);
   const fq6d r0 = fq6d_sub(fq6d_sub(Q, P), fq6d_mul_v(P));
   const fq6d r1 = fq6d_add(Q, Q);
@@ -671,6 +675,125 @@ __device__ __forceinline__ fqd point_scalar2d(const g1a& P, bool neg, bool l1) {
   const fq y = neg ? fq_neg(P.y) : P.y;
   const fq yi = fq_inv_i(y);
   return fqd_from_fq(l1 ? fq_mul(P.x, yi) : yi);
+}
+
+// ---- the coin's check: lines generated on the fly, f split over the pair ----------------------
+// A lane's LDS words: its own line c0 + c1 v + c4 v w (c4 in Fq2: an un-normalised line at a G1
+// point; packed, words 0..77), and one packed park (words MG_PARK..155) holding whichever of T and
+// f is idle -- T while the pair multiplies, f while the lane generates its line.  The squaring
+// uses words 0..55 (sqr2d<true>).  In registers at any time: f or T, and one step's temporaries.
+constexpr int MG_PARK = 78;
+
+// f * (c0 + c1 v + c4 v w) with the packed line in the lane column `ln` (either lane of the pair):
+// lane 0 A0 L0 + v^2 c4 A1, lane 1 A1 L0 + v c4 A0 (L0 = c0 + c1 v; w^2 = v).  8 Fq2 products per
+// lane against the one-lane sparse product's 13; the partner's half comes over one coefficient at
+// a time.  Reduced output.
+__device__ __forceinline__ fq6d line2d_f2(const fq6d& A, bool l1, const lds_u32* ln) {
+  fq6d acc;  // v^(2-k) c4 A_(1-k), then + A_k L0 (fieldd.hpp fq6d_mul_by_01's Karatsuba)
+  {
+    const fq2d c4 = slot_get_fq2d(ln, 64u, 2);
+    fq6d E;
+    E.c0 = fq2d_mul(xchg_t(A.c0), c4);
+    HBX_SEQ();
+    E.c1 = fq2d_mul(xchg_t(A.c1), c4);
+    HBX_SEQ();
+    E.c2 = fq2d_mul(xchg_t(A.c2), c4);
+    const fq6d vE = fq6d_mul_v(E);
+    acc = sel_t(l1, vE, fq6d_mul_v(vE));
+  }
+  HBX_SEQ();
+  const fq2d c0 = slot_get_fq2d(ln, 64u, 0), c1 = slot_get_fq2d(ln, 64u, 1);
+  {
+    const fq2d t0 = fq2d_mul(A.c0, c0);
+    acc.c0 = fq2d_add(acc.c0, t0);
+    acc.c1 = fq2d_sub(acc.c1, t0);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(A.c1, c1);
+    acc.c1 = fq2d_sub(acc.c1, t1);
+    acc.c2 = fq2d_add(acc.c2, t1);
+  }
+  HBX_SEQ();
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(A.c2, c1)));
+  HBX_SEQ();
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(A.c0, A.c1), fq2d_add(c0, c1)));
+  HBX_SEQ();
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(A.c2, c0));
+  HBX_SEQ();
+  return fq6d_reduce(acc);  // digit sums of a few normalised values: below 2^31
+}
+
+// The coin check's two Miller loops on a pair (pairingd.hpp miller_loop_gen_parked_d, both pairs):
+// lane k generates the lines of its own pair (Q = *q, P = (px, py); lane 0 (H', pk_i), lane 1
+// (sigma_i, -[m] g1)) into its LDS words, and the pair multiplies the split f by lane 0's line and
+// then lane 1's.  Returns this lane's half of f_A f_B, conjugated for x < 0; T = [|x|] Q.  An
+// unused pair (`use` false: a point at infinity) contributes lines equal to 1.  The one-lane loop
+// held a whole Fq12 plus the sparse product's temporaries per lane and spilled (367 VGPRs,
+// 10.6 GB of scratch traffic per coin launch).
+__device__ __forceinline__ fq6d miller_gen2d(const g2a* q, const fqd& px, const fqd& py, bool use, bool l1, lds2 lds,
+                                             const lds_u32* pair0, g2jd& Tout) {
+  const fq2d one{fqd_const(FQD_ONE), fqd_zero()}, zero{fqd_zero(), fqd_zero()};
+  lds_u32* park = lds + MG_PARK * 64;
+  {
+    const g2a Q = *q;
+    slot_put_fq6d(park, 64u, fq6d{fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), one});  // T
+  }
+  fq6d f = sel_t(l1, fq6d_zero(), fq6d_one());
+  // one line step: T from the park, f to it, the line (doubling, or addition of Q), f back, T to
+  // the park, the pair's two line products
+  auto step = [&](bool add) __attribute__((always_inline)) {
+    HBX_SEQ();
+    g2jd T;
+    {
+      const fq6d t = slot_get_fq6d(park, 64u);
+      T = g2jd{t.c0, t.c1, t.c2};
+    }
+    HBX_SEQ();
+    slot_put_fq6d(park, 64u, f);
+    HBX_SEQ();
+    fq2d c0, c1, c2;
+    if (!add) {
+      line_dbl_step_di(T, c0, c1, c2);
+    } else {
+      const g2a Q = *q;  // the five addition steps re-read the base point
+      line_add_step_call(T, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), c0, c1, c2);
+    }
+    HBX_SEQ();
+    slot_put_fq2d(lds, 64u, 0, sel_t(use, c0, one));
+    slot_put_fq2d(lds, 64u, 1, sel_t(use, fq2d_mul_fq(c1, px), zero));
+    slot_put_fq2d(lds, 64u, 2, sel_t(use, fq2d_mul_fq(c2, py), zero));
+    HBX_SEQ();
+    f = slot_get_fq6d(park, 64u);
+    HBX_SEQ();
+    slot_put_fq6d(park, 64u, fq6d{T.x, T.y, T.z});
+    HBX_SEQ();
+    f = line2d_f2(f, l1, pair0);
+    HBX_SEQ();
+    f = line2d_f2(f, l1, pair0 + 1);
+  };
+  // |x| = 0xd201000000010000: the doubling steps i = 62..0 in runs, an addition step after each run
+  // but the last (bits 62, 60, 57, 48, 16).  The addition is an out-of-line call, kept out of the
+  // runs' loops: inside the loop the values live across it spilled (139 VGPRs).
+  static_assert(BLS_X == 0xd201000000010000ull, "the runs below follow |x|'s bits");
+  constexpr int RUN[6] = {1, 2, 3, 9, 32, 16};
+  bool first = true;
+#pragma unroll 1
+  for (int r = 0; r < 6; r++) {
+#pragma unroll 1
+    for (int t = 0; t < RUN[r]; t++) {
+      if (!first) f = sqr2d<true>(f, l1, lds);
+      first = false;
+      step(false);
+    }
+    if (r < 5) step(true);
+  }
+  HBX_SEQ();
+  {
+    const fq6d t = slot_get_fq6d(park, 64u);
+    Tout = g2jd{t.c0, t.c1, t.c2};
+  }
+  return conj2d(f, l1);
 }
 
 // ---- the whole check ------------------------------------------------------------------------

@@ -69,7 +69,7 @@ HBX_HD void line_dbl_step_di(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) {
 HBX_HDNI void line_dbl_step_d(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2) { line_dbl_step_di(T, c0, c1, c2); }
 // Raw line through T and the affine base point (qx, qy), scaled by den = Z (X - xQ Z^2):
 // c0 = num xQ - yQ den, c1 = -num, c2 = den;  T <- T + Q (madd-2007-bl).
-HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
+HBX_HD void line_add_step_di(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
   const fq2d Z1Z1 = fq2d_sqr(T.z);
   const fq2d U2 = fq2d_mul(qx, Z1Z1);
   const fq2d S2 = fq2d_mul(fq2d_mul(qy, T.z), Z1Z1);
@@ -88,6 +88,22 @@ HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0,
   const fq2d Y3 = fq2d_reduce(fq2d_sub(fq2d_mul(r, fq2d_sub(V, X3)), fq2d_dbl(fq2d_mul(T.y, J))));
   const fq2d Z3 = fq2d_reduce(fq2d_sub(fq2d_sub(fq2d_sqr(fq2d_norm(fq2d_add(T.z, H))), Z1Z1), HH));
   T = g2jd{X3, Y3, Z3};
+}
+HBX_HDNI void line_add_step_d(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
+  line_add_step_di(T, qx, qy, c0, c1, c2);
+}
+// The out-of-line addition step called from a loop that keeps T and the line in registers: through
+// copies, so that only the copies' addresses escape into the call.  Passing the loop's own T and
+// line by reference kept them in scratch memory across the whole loop -- every doubling step read
+// and wrote T there (the coin Miller kernel's 6.6 GB of scratch traffic per launch).
+HBX_HD void line_add_step_call(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1, fq2d& c2) {
+  g2jd t = T;
+  fq2d a0, a1, a2;
+  line_add_step_d(t, qx, qy, a0, a1, a2);
+  T = t;
+  c0 = a0;
+  c1 = a1;
+  c2 = a2;
 }
 // f * (c0 + c1 v + c4 v w) with c4 in Fq2 (an un-normalised line at a G1 point)
 HBX_HD fq12d fq12d_mul_by_014_f2_i(const fq12d& f, const fq2d& c0, const fq2d& c1, const fq2d& c4) {
@@ -122,7 +138,7 @@ HBX_HDNI fq12d miller_loop_mixed_d(const line_pre_d* LA, const fqd& ax, const fq
       if (useB) {
         fq2d c0, c1, c2;
         if (s == 0) line_dbl_step_d(T, c0, c1, c2);
-        else line_add_step_d(T, qx, qy, c0, c1, c2);
+        else line_add_step_call(T, qx, qy, c0, c1, c2);
         f = fq12d_mul_by_014_f2(f, c0, fq2d_mul_fq(c1, bx), fq2d_mul_fq(c2, by));
       }
       k++;
@@ -146,7 +162,7 @@ HBX_HD fq12d miller_loop_gen_d(const fq2d& qx, const fq2d& qy, const fqd& bx, co
     for (int s = 0; s < (((BLS_X >> i) & 1) ? 2 : 1); s++) {
       fq2d c0, c1, c2;
       if (s == 0) line_dbl_step_di(T, c0, c1, c2);
-      else line_add_step_d(T, qx, qy, c0, c1, c2);
+      else line_add_step_call(T, qx, qy, c0, c1, c2);
       HBX_SEQ();
       f = fq12d_mul_by_014_f2_i(f, c0, fq2d_mul_fq(c1, bx), fq2d_mul_fq(c2, by));
       HBX_SEQ();
@@ -366,7 +382,7 @@ HBX_HD fq12d miller_loop_gen_parked_d(const fq2d& qx, const fq2d& qy, const fqd&
         line_dbl_step_di(T, c0, c1, c2);
       } else {
         const fq2d px{park_get_fqd(park, 0), park_get_fqd(park, 1)}, py{park_get_fqd(park, 2), park_get_fqd(park, 3)};
-        line_add_step_d(T, px, py, c0, c1, c2);
+        line_add_step_call(T, px, py, c0, c1, c2);
       }
       HBX_SEQ();
       const fqd ex = park_get_fqd(park, 4), ey = park_get_fqd(park, 5);

@@ -1,7 +1,7 @@
 """HBM bytes per launch of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE), as
 the JSON record bench.py's `traffic` field reads (profiles/<tag>_pmc_hbm.json).
 
-    python tools/pmc_json.py <fetch results.db> <write results.db> <kernel>[,<kernel>...] <commit> > out.json
+    python tools/pmc_json.py <fetch results.db> <write results.db> <kernel>[,<kernel>...] <commit> [--skip-empty] > out.json
 
 Several comma-separated kernel names make one region (the one-lane share check is the Miller
 kernel + seven step kernels + the fallback launch): its bytes are the sum of each kernel's bytes
@@ -17,18 +17,25 @@ import sqlite3
 import sys
 
 
+SKIP_EMPTY = "--skip-empty" in sys.argv  # launches that return at once (a retry pass with nothing
+                                        # to retry) are not launches of the region
+
+
 def per_launch(db, counter, kernel):
     c = sqlite3.connect(db)
-    q = ("select sum(value), count(distinct dispatch_id) from counters_collection "
-         "where counter_name = ? and kernel_name like ?")
-    v, nd = c.execute(q, (counter, f"%{kernel}%")).fetchone()
-    if not nd:
+    q = ("select dispatch_id, sum(value) from counters_collection "
+         "where counter_name = ? and kernel_name like ? group by dispatch_id")
+    vals = [v for _, v in c.execute(q, (counter, f"%{kernel}%")).fetchall()]
+    if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} in {db}")
-    return v / nd, nd
+    if SKIP_EMPTY:
+        top = max(vals)
+        vals = [v for v in vals if v > 0.01 * top] or vals
+    return sum(vals) / len(vals), len(vals)
 
 
 def main():
-    fdb, wdb, kernel, commit = sys.argv[1:5]
+    fdb, wdb, kernel, commit = [a for a in sys.argv[1:] if not a.startswith("--")][:4]
     f_kib = w_kib = 0.0
     nf, nw = [], []
     parts = {}
