@@ -153,11 +153,12 @@ def hbx_build_info():
     return hbx.build_info()
 
 
-def traffic_record():
-    """Newest PMC record for the share check (profiles/*_pmc_hbm.json), or None."""
+def traffic_record(kind="hbm"):
+    """Newest PMC record for the share check (profiles/*_pmc_hbm.json) or the coin's two-lane
+    signature-share check (kind "coin": profiles/*_pmc_coin.json), or None."""
     import glob
 
-    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_hbm.json")))
+    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kind}.json")))
     if not recs:
         return None
     with open(recs[-1]) as fh:
@@ -646,6 +647,13 @@ def config_c4(args, dev, torch, Context):
                         "kernel_ms": kms,
                         "work": f"{inst * n} checks x {VSIG_FQMUL} Fq-mul (frozen unit V_sig) x {MADS_PER_FQMUL} MAD",
                         "opcount": {"fqmul_per_check": OPCOUNT_VSIG, "frac": round(achieved_op / PEAK_TMAD_S, 4)}}}
+    coin_pmc = traffic_record("coin") if lanes == 2 else None
+    if coin_pmc:
+        res["roofline"]["traffic"] = coin_pmc["bytes_per_launch"]
+        res["roofline"]["traffic_note"] = (
+            f"PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch of {coin_pmc['kernel']} at this workload "
+            f"({coin_pmc['source']}, commit {coin_pmc.get('commit', '?')}); algorithmic: the keys, H', the "
+            f"decoded shares and one Fq12 per check written to and read from the pair's global slot (~0.05e9 B)")
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_coin(pk, nonces, bad, corrupt, master_pk, t, args.cpu_seconds)
     return res
