@@ -26,7 +26,7 @@ namespace hbx {
 
 // lane K of the calling lane's 16-lane row, to every lane of the row (DPP row_newbcast per digit).
 // Each moved digit is pinned in a register (HBX_LAUNDER) so the compiler cannot fold the move into
-// its consumer as a DPP-modified add / subtract: in the fqd_pick addition such folded row_newbcast
+// its consumer as a DPP-modified add / subtract: in the group addition such folded row_newbcast
 // operations produced wrong sums on gfx950 (tools/microbench/addcmp.hip: Y1 Z2 differed from the
 // same expression outside the function; with the moves pinned both agree and the hash-to-G2
 // checksum of profiles/r05o_hashg2.txt is reproduced).
@@ -53,26 +53,37 @@ __device__ __forceinline__ fqd fqd_sel8(int s, const fqd& v0, const fqd& v1, con
   }
   return r;
 }
-// a lane's operand among 16 candidates given as separate values (a 16-entry candidate array --
-// two per round -- was kept in scratch memory: 1,093 scratch accesses per addition)
-__device__ __forceinline__ int32_t pick_digit(int, int, int, int32_t t) { return t; }
-template <class... R>
-__device__ __forceinline__ int32_t pick_digit(int s, int i, int k, int32_t t, const fqd& v, const R&... rest) {
-  return pick_digit(s, i, k + 1, s == k ? v.d[i] : t, rest...);
+// One product round on a 16-lane group from eight two-lane blocks: block b (lanes 2b, 2b + 1) is
+// a square of X_b (SQ bit b set: lanes ((a0 + a1)(a0 - a1), a0 a1)) or half of a schoolbook product
+// X_b Y_b spanning the 4-aligned blocks 2c, 2c + 1 (lanes a0 b0, a1 b1, a0 b1, a1 b0).  A lane first
+// selects its block's X and Y among values that are live anyway (a three-level select tree, like
+// the doubling's fqd_sel8), then forms its operands: a 16-entry candidate list per operand -- the
+// square sums materialised for every block -- held ~450 registers at once and spilled (~600
+// scratch accesses per addition).
+__device__ __forceinline__ fq2d fq2d_sel8(int s, const fq2d& v0, const fq2d& v1, const fq2d& v2, const fq2d& v3,
+                                          const fq2d& v4, const fq2d& v5, const fq2d& v6, const fq2d& v7) {
+  return fq2d{fqd_sel8(s, v0.c0, v1.c0, v2.c0, v3.c0, v4.c0, v5.c0, v6.c0, v7.c0),
+              fqd_sel8(s, v0.c1, v1.c1, v2.c1, v3.c1, v4.c1, v5.c1, v6.c1, v7.c1)};
 }
-template <class... R>
-__device__ __forceinline__ fqd fqd_pick(int s, const fqd& v0, const R&... rest) {
-  static_assert(sizeof...(R) == 15, "16 candidates");
-  fqd r;
+template <uint32_t SQ>
+__device__ __forceinline__ fqd gd_round(int gl, const fq2d& x0, const fq2d& x1, const fq2d& x2, const fq2d& x3,
+                                        const fq2d& x4, const fq2d& x5, const fq2d& x6, const fq2d& x7,
+                                        const fq2d& y0, const fq2d& y1, const fq2d& y2, const fq2d& y3,
+                                        const fq2d& y4, const fq2d& y5, const fq2d& y6, const fq2d& y7) {
+  const int blk = (gl >> 1) & 7, sub = gl & 3;
+  const bool sq = ((SQ >> blk) & 1) != 0;
+  const fq2d X = fq2d_sel8(blk, x0, x1, x2, x3, x4, x5, x6, x7);
+  const fq2d Y = fq2d_sel8(blk, y0, y1, y2, y3, y4, y5, y6, y7);
+  fqd a, b;
 #pragma unroll
-  for (int i = 0; i < 14; i++) r.d[i] = pick_digit(s, i, 1, v0.d[i], rest...);
-  return r;
+  for (int i = 0; i < 14; i++) {
+    const int32_t x0d = X.c0.d[i], x1d = X.c1.d[i], y0d = Y.c0.d[i], y1d = Y.c1.d[i];
+    // square lanes: (x0 + x1, x0 - x1) | (x0, x1); product lanes: (x0, y0) (x1, y1) (x0, y1) (x1, y0)
+    a.d[i] = sq ? ((gl & 1) ? x0d : x0d + x1d) : ((sub & 1) ? x1d : x0d);
+    b.d[i] = sq ? ((gl & 1) ? x1d : x0d - x1d) : ((sub == 1 || sub == 2) ? y1d : y0d);
+  }
+  return fqd_mul(a, b);
 }
-// candidate lists of one Fq2 product (4 lanes, schoolbook) or square (2 lanes)
-#define GD_MULA(x) (x).c0, (x).c1, (x).c0, (x).c1
-#define GD_MULB(y) (y).c0, (y).c1, (y).c1, (y).c0
-#define GD_SQRA(x) fqd_add((x).c0, (x).c1), (x).c0
-#define GD_SQRB(x) fqd_sub((x).c0, (x).c1), (x).c1
 
 // Fq2 results of a round: a square from rows (K, K + 1) = ((a0 + a1)(a0 - a1), a0 a1), a product
 // from rows (K .. K + 3) = (a0 b0, a1 b1, a0 b1, a1 b0) (schoolbook).  Digits below 2^29.
@@ -117,20 +128,18 @@ __device__ __forceinline__ g2jd g2d_dbl_n_group(g2jd p, int n, int gl) {
 __device__ __forceinline__ g2jd g2d_add_group_i(const g2jd& p, const g2jd& q, int gl) {
   if (fq2d_is_zero_mod(p.z)) return q;
   if (fq2d_is_zero_mod(q.z)) return p;
-  const fqd z = fqd_zero();
+  const fq2d z{fqd_zero(), fqd_zero()};
   // round 1: Z1^2 (0, 1), Z2^2 (2, 3), Y1 Z2 (4..7), Y2 Z1 (8..11), (Z1 + Z2)^2 (12, 13)
   fqd r;
   {
     const fq2d zs = fq2d_relax(fq2d_add(p.z, q.z));
-    r = fqd_mul(fqd_pick(gl, GD_SQRA(p.z), GD_SQRA(q.z), GD_MULA(p.y), GD_MULA(q.y), GD_SQRA(zs), z, z),
-                fqd_pick(gl, GD_SQRB(p.z), GD_SQRB(q.z), GD_MULB(q.z), GD_MULB(p.z), GD_SQRB(zs), z, z));
+    r = gd_round<0x43>(gl, p.z, q.z, p.y, p.y, q.y, q.y, zs, z, p.z, q.z, q.z, q.z, p.z, p.z, zs, z);
   }
   const fq2d Z1Z1 = rows_sqr<0>(r), Z2Z2 = rows_sqr<2>(r);
   const fq2d Y1Z2 = rows_mul<4>(r), Y2Z1 = rows_mul<8>(r);
   const fq2d ZS = rows_sqr<12>(r);
   // round 2: U1 (0..3), U2 (4..7), S1 (8..11), S2 (12..15)
-  r = fqd_mul(fqd_pick(gl, GD_MULA(p.x), GD_MULA(q.x), GD_MULA(Y1Z2), GD_MULA(Y2Z1)),
-              fqd_pick(gl, GD_MULB(Z2Z2), GD_MULB(Z1Z1), GD_MULB(Z2Z2), GD_MULB(Z1Z1)));
+  r = gd_round<0>(gl, p.x, p.x, q.x, q.x, Y1Z2, Y1Z2, Y2Z1, Y2Z1, Z2Z2, Z2Z2, Z1Z1, Z1Z1, Z2Z2, Z2Z2, Z1Z1, Z1Z1);
   const fq2d U1 = rows_mul<0>(r), S1 = rows_mul<8>(r);
   const fq2d H = fq2d_relax(fq2d_sub(rows_mul<4>(r), U1));
   const fq2d dS = fq2d_relax(fq2d_sub(rows_mul<12>(r), S1));
@@ -142,22 +151,19 @@ __device__ __forceinline__ g2jd g2d_add_group_i(const g2jd& p, const g2jd& q, in
   // round 3: H^2 (0, 1), dS^2 (2, 3), ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H (4..7)
   {
     const fq2d zz = fq2d_relax(fq2d_sub(fq2d_sub(ZS, Z1Z1), Z2Z2));
-    r = fqd_mul(fqd_pick(gl, GD_SQRA(H), GD_SQRA(dS), GD_MULA(zz), z, z, z, z, z, z, z, z),
-                fqd_pick(gl, GD_SQRB(H), GD_SQRB(dS), GD_MULB(H), z, z, z, z, z, z, z, z));
+    r = gd_round<0x03>(gl, H, dS, zz, zz, z, z, z, z, H, dS, H, H, z, z, z, z);
   }
   const fq2d I = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<0>(r))));   // (2H)^2
   const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<2>(r))));  // rr^2
   const fq2d Z3 = fq2d_relax(rows_mul<4>(r));
   // round 4: J = H I (0..3), V = U1 I (4..7)
-  r = fqd_mul(fqd_pick(gl, GD_MULA(H), GD_MULA(U1), z, z, z, z, z, z, z, z),
-              fqd_pick(gl, GD_MULB(I), GD_MULB(I), z, z, z, z, z, z, z, z));
+  r = gd_round<0>(gl, H, H, U1, U1, z, z, z, z, I, I, I, I, z, z, z, z);
   const fq2d J = rows_mul<0>(r), V = rows_mul<4>(r);
   const fq2d X3 = fq2d_relax(fq2d_sub(fq2d_relax(fq2d_sub(RR, J)), fq2d_dbl(V)));
   // round 5: rr (V - X3) (0..3), S1 J (4..7)
   {
     const fq2d w = fq2d_sub(V, X3);
-    r = fqd_mul(fqd_pick(gl, GD_MULA(rr), GD_MULA(S1), z, z, z, z, z, z, z, z),
-                fqd_pick(gl, GD_MULB(w), GD_MULB(J), z, z, z, z, z, z, z, z));
+    r = gd_round<0>(gl, rr, rr, S1, S1, z, z, z, z, w, w, J, J, z, z, z, z);
   }
   const fq2d Y3 = fq2d_relax(fq2d_sub(rows_mul<0>(r), fq2d_dbl(rows_mul<4>(r))));
   return g2jd{X3, Y3, Z3};
@@ -225,23 +231,22 @@ __device__ __noinline__ g2jd g2d_clear_cofactor_group(const g2jd& P, int gl, boo
 // Relaxed in and out (T and the line's coefficients).
 __device__ __forceinline__ void line_dbl_step_groupd(g2jd& T, fq2d& c0, fq2d& c1, fq2d& c2, int gl) {
   const fqd x0 = T.x.c0, x1 = T.x.c1, y0 = T.y.c0, y1 = T.y.c1, z0 = T.z.c0, z1 = T.z.c1;
-  const fqd z = fqd_zero();
-  fqd r = fqd_mul(fqd_pick(gl, GD_SQRA(T.x), GD_SQRA(T.y), GD_SQRA(T.z), GD_MULA(T.y), z, z, z, z, z, z),
-                  fqd_pick(gl, GD_SQRB(T.x), GD_SQRB(T.y), GD_SQRB(T.z), GD_MULB(T.z), z, z, z, z, z, z));
-  const fq2d A = rows_sqr<0>(r), B = rows_sqr<2>(r), ZZ = rows_sqr<4>(r), YZ = rows_mul<6>(r);
+  const fq2d z{fqd_zero(), fqd_zero()};
+  // X^2 (0, 1), Y^2 (2, 3), Z^2 (4, 5), Y Z (8..11)
+  fqd r = gd_round<0x07>(gl, T.x, T.y, T.z, z, T.y, T.y, z, z, T.x, T.y, T.z, z, T.z, T.z, z, z);
+  const fq2d A = rows_sqr<0>(r), B = rows_sqr<2>(r), ZZ = rows_sqr<4>(r), YZ = rows_mul<8>(r);
   const fq2d E = fq2d_relax(fq2d_add(fq2d_dbl(A), A));
   const fq2d S = fq2d_relax(fq2d_add(T.x, B));
-  r = fqd_mul(fqd_pick(gl, GD_SQRA(B), GD_SQRA(S), GD_SQRA(E), GD_MULA(E), GD_MULA(E), z, z),
-              fqd_pick(gl, GD_SQRB(B), GD_SQRB(S), GD_SQRB(E), GD_MULB(T.x), GD_MULB(ZZ), z, z));
-  const fq2d C = rows_sqr<0>(r), TT = rows_sqr<2>(r), F = rows_sqr<4>(r), EX = rows_mul<6>(r), EZZ = rows_mul<10>(r);
+  // B^2 (0, 1), S^2 (2, 3), E^2 (4, 5), E X (8..11), E Z^2 (12..15)
+  r = gd_round<0x07>(gl, B, S, E, z, E, E, E, E, B, S, E, z, T.x, T.x, ZZ, ZZ);
+  const fq2d C = rows_sqr<0>(r), TT = rows_sqr<2>(r), F = rows_sqr<4>(r), EX = rows_mul<8>(r), EZZ = rows_mul<12>(r);
   c0 = fq2d_relax(fq2d_sub(EX, fq2d_dbl(B)));
   c1 = fq2d_relax(fq2d_neg(EZZ));
   const fq2d D = fq2d_dbl(fq2d_relax(fq2d_sub(fq2d_sub(TT, A), C)));
   const fq2d X3 = fq2d_relax(fq2d_sub(F, fq2d_dbl(D)));
   const fq2d Z3 = fq2d_relax(fq2d_dbl(YZ));
   const fq2d G = fq2d_sub(D, X3);
-  r = fqd_mul(fqd_pick(gl, GD_MULA(E), GD_MULA(Z3), z, z, z, z, z, z, z, z),
-              fqd_pick(gl, GD_MULB(G), GD_MULB(ZZ), z, z, z, z, z, z, z, z));
+  r = gd_round<0>(gl, E, E, Z3, Z3, z, z, z, z, G, G, ZZ, ZZ, z, z, z, z);
   const fq2d EG = rows_mul<0>(r);
   c2 = fq2d_relax(rows_mul<4>(r));
   const fq2d C8 = fq2d_dbl(fq2d_dbl(fq2d_relax(fq2d_dbl(C))));
@@ -253,38 +258,33 @@ __device__ __forceinline__ void line_dbl_step_groupd(g2jd& T, fq2d& c0, fq2d& c1
 // the 16 lanes of a group in five rounds.  T relaxed in and out; (qx, qy) normalised.
 __device__ __forceinline__ void line_add_step_groupd(g2jd& T, const fq2d& qx, const fq2d& qy, fq2d& c0, fq2d& c1,
                                                      fq2d& c2, int gl) {
-  const fqd z = fqd_zero();
-  // round 1: Z1Z1 = Z^2 (0, 1), yQ Z (2..5)
-  fqd r = fqd_mul(fqd_pick(gl, GD_SQRA(T.z), GD_MULA(qy), z, z, z, z, z, z, z, z, z, z),
-                  fqd_pick(gl, GD_SQRB(T.z), GD_MULB(T.z), z, z, z, z, z, z, z, z, z, z));
-  const fq2d Z1Z1 = rows_sqr<0>(r), YqZ = rows_mul<2>(r);
+  const fq2d z{fqd_zero(), fqd_zero()};
+  // round 1: Z1Z1 = Z^2 (0, 1), yQ Z (4..7)
+  fqd r = gd_round<0x01>(gl, T.z, z, qy, qy, z, z, z, z, T.z, z, T.z, T.z, z, z, z, z);
+  const fq2d Z1Z1 = rows_sqr<0>(r), YqZ = rows_mul<4>(r);
   // round 2: U2 = xQ Z1Z1 (0..3), S2 = yQ Z Z1Z1 (4..7)
-  r = fqd_mul(fqd_pick(gl, GD_MULA(qx), GD_MULA(YqZ), z, z, z, z, z, z, z, z),
-              fqd_pick(gl, GD_MULB(Z1Z1), GD_MULB(Z1Z1), z, z, z, z, z, z, z, z));
+  r = gd_round<0>(gl, qx, qx, YqZ, YqZ, z, z, z, z, Z1Z1, Z1Z1, Z1Z1, Z1Z1, z, z, z, z);
   const fq2d H = fq2d_relax(fq2d_sub(rows_mul<0>(r), T.x));  // -(X - xQ Z^2)
   const fq2d num = fq2d_relax(fq2d_sub(T.y, rows_mul<4>(r)));
-  // round 3: Z H (0..3), H^2 (4, 5), num xQ (6..9), num^2 (10, 11), (Z + H)^2 (12, 13)
+  // round 3: Z H (0..3), H^2 (4, 5), num^2 (6, 7), num xQ (8..11), (Z + H)^2 (12, 13)
   {
     const fq2d zh = fq2d_relax(fq2d_add(T.z, H));
-    r = fqd_mul(fqd_pick(gl, GD_MULA(T.z), GD_SQRA(H), GD_MULA(num), GD_SQRA(num), GD_SQRA(zh), z, z),
-                fqd_pick(gl, GD_MULB(H), GD_SQRB(H), GD_MULB(qx), GD_SQRB(num), GD_SQRB(zh), z, z));
+    r = gd_round<0x4C>(gl, T.z, T.z, H, num, num, num, zh, z, H, H, H, num, qx, qx, zh, z);
   }
   c2 = fq2d_relax(fq2d_neg(rows_mul<0>(r)));  // den
-  const fq2d HH = rows_sqr<4>(r), NX = rows_mul<6>(r), ZHs = rows_sqr<12>(r);
-  const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<10>(r))));  // rr^2 = 4 num^2
+  const fq2d HH = rows_sqr<4>(r), NX = rows_mul<8>(r), ZHs = rows_sqr<12>(r);
+  const fq2d RR = fq2d_dbl(fq2d_relax(fq2d_dbl(rows_sqr<6>(r))));  // rr^2 = 4 num^2
   const fq2d I = fq2d_dbl(fq2d_relax(fq2d_dbl(HH)));
   c1 = fq2d_relax(fq2d_neg(num));
   // round 4: yQ den (0..3), J = H I (4..7), V = X I (8..11)
-  r = fqd_mul(fqd_pick(gl, GD_MULA(qy), GD_MULA(H), GD_MULA(T.x), z, z, z, z),
-              fqd_pick(gl, GD_MULB(c2), GD_MULB(I), GD_MULB(I), z, z, z, z));
+  r = gd_round<0>(gl, qy, qy, H, H, T.x, T.x, z, z, c2, c2, I, I, I, I, z, z);
   c0 = fq2d_relax(fq2d_sub(NX, rows_mul<0>(r)));
   const fq2d J = rows_mul<4>(r), V = rows_mul<8>(r);
   const fq2d X3 = fq2d_relax(fq2d_sub(fq2d_relax(fq2d_sub(RR, J)), fq2d_dbl(V)));
   // round 5: rr (V - X3) with rr = 2 (S2 - Y) = -2 num (0..3), Y J (4..7)
   {
     const fq2d rr = fq2d_dbl(c1), w = fq2d_sub(V, X3);
-    r = fqd_mul(fqd_pick(gl, GD_MULA(rr), GD_MULA(T.y), z, z, z, z, z, z, z, z),
-                fqd_pick(gl, GD_MULB(w), GD_MULB(J), z, z, z, z, z, z, z, z));
+    r = gd_round<0>(gl, rr, rr, T.y, T.y, z, z, z, z, w, w, J, J, z, z, z, z);
   }
   const fq2d Y3 = fq2d_relax(fq2d_sub(rows_mul<0>(r), fq2d_dbl(rows_mul<4>(r))));
   T = g2jd{X3, Y3, fq2d_relax(fq2d_sub(fq2d_sub(ZHs, Z1Z1), HH))};
