@@ -58,6 +58,59 @@ HBX_HD g1jd g1d_add_mixed(const g1jd& p, const fqd& qx, const fqd& qy) {
   return g1jd{X3, Y3, Z3};
 }
 
+// p + q, add-2007-bl (curve.hpp g1_add_i) without its special cases: for operands that are
+// neither the identity nor equal or opposite (the window additions below).  Relaxed in and out.
+HBX_HD g1jd g1d_add_nc(const g1jd& p, const g1jd& q) {
+  const fqd Z1Z1 = fqd_sqr(p.z);
+  const fqd Z2Z2 = fqd_sqr(q.z);
+  const fqd U1 = fqd_mul(p.x, Z2Z2);
+  const fqd U2 = fqd_mul(q.x, Z1Z1);
+  const fqd S1 = fqd_mul(fqd_mul(p.y, q.z), Z2Z2);
+  const fqd S2 = fqd_mul(fqd_mul(q.y, p.z), Z1Z1);
+  const fqd H = fqd_relax(fqd_sub(U2, U1));
+  const fqd I = fqd_sqr(fqd_dbl(H));
+  const fqd J = fqd_mul(H, I);
+  const fqd r = fqd_dbl(fqd_relax(fqd_sub(S2, S1)));
+  const fqd V = fqd_mul(U1, I);
+  const fqd X3 = fqd_relax(fqd_sub(fqd_sub(fqd_sqr(r), J), fqd_dbl(V)));
+  const fqd Y3 = fqd_relax(fqd_sub(fqd_mul(r, fqd_sub(V, X3)), fqd_dbl(fqd_mul(S1, J))));
+  const fqd Z3 = fqd_mul(fqd_relax(fqd_sub(fqd_sub(fqd_sqr(fqd_relax(fqd_add(p.z, q.z))), Z1Z1), Z2Z2)), H);
+  return g1jd{X3, Y3, Z3};
+}
+
+// curve.hpp g1_mul_u128_w4 (the threshold combine's GLV halves: 4-bit fixed windows, the table
+// (1..15) P in per-lane scratch) with the point arithmetic in the digit tower.  P has prime order
+// r > 2^128, so a window addition adds m P and n P with 16 <= m, 1 <= n <= 15, m + n < r: never
+// equal or opposite points; the accumulator is the identity exactly while the scalar's leading
+// windows are zero (a flag, as g2d.hpp g2d_mul_u64_w4_t does).  The same point as the 12-limb
+// version (tests/test_hostcheck.py::test_g1_mul_u128_digit_tower).
+HBX_HDNI g1j g1d_mul_u128_w4(const g1a& P, const uint32_t* k4) {
+  if (P.inf) return g1_identity();
+  const fqd px = fqd_from_fq(P.x), py = fqd_from_fq(P.y);
+  g1jd tab[16];
+  tab[0] = g1jd{fqd_const(FQD_ONE), fqd_const(FQD_ONE), fqd_zero()};
+  tab[1] = g1jd{px, py, fqd_const(FQD_ONE)};
+#pragma unroll 1
+  for (int i = 2; i < 16; i++) tab[i] = g1d_add_mixed(tab[i - 1], px, py);
+  const uint32_t top = k4[3] >> 28;
+  g1jd acc = tab[top];
+  bool ai = top == 0;
+#pragma unroll 1
+  for (int w = 30; w >= 0; w--) {
+    const uint32_t nib = (k4[w >> 3] >> ((w & 7) * 4)) & 0xFu;
+    if (!ai) {
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) acc = g1d_dbl(acc);
+    }
+    if (nib) {
+      acc = ai ? tab[nib] : g1d_add_nc(acc, tab[nib]);
+      ai = false;
+    }
+  }
+  if (ai) return g1_identity();
+  return g1j{fqd_to_fq(acc.x), fqd_to_fq(acc.y), fqd_to_fq(acc.z)};
+}
+
 // P in G1 for an affine point on the curve (curve.hpp g1_is_torsion_free, the same criterion)
 HBX_HDNI bool g1_is_torsion_free_d(const g1a& P) {
   if (P.inf) return true;

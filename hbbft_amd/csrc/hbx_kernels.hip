@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(COMBINE_THREADS) k_combine(const uint8_t* __re
     g1_glv_split(lam.l, k1, k2);
     g1a sp = S[(size_t)j * n + idx[k]];
     if (q & 1) sp.x = fq_mul(sp.x, fq_from_const(G1_BETA));
-    acc = g1_add(acc, g1_mul_u128_w4(sp, (q & 1) ? k2 : k1));
+    acc = g1_add(acc, g1d_mul_u128_w4(sp, (q & 1) ? k2 : k1));  // digit tower (g1d.hpp)
   }
   red[tid] = acc;
   __syncthreads();

@@ -506,6 +506,18 @@ def test_g2_mul_u64_windows_match_naf(hc):
         assert hc.hc_g2_mul_u64_cmp(q, k) == 1, hex(k)
 
 
+def test_g1_mul_u128_digit_tower(hc):
+    """k_combine's GLV-half G1 multiplications in the digit tower (g1d.hpp g1d_mul_u128_w4) equal
+    the 12-limb windowed ones, zero and single-window scalars included."""
+    hc.hc_g1_mul_u128_cmp.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32)]
+    rnd = random.Random(31)
+    p = bls.g1_compress(bls.g1_mul(bls.G1_GEN, rnd.randrange(1, bls.R)))
+    ks = [0, 1, 2, 15, 16, 17, 1 << 124, (1 << 128) - 1, 0xF << 124] + [rnd.getrandbits(128) for _ in range(6)]
+    for k in ks:
+        k4 = (ctypes.c_uint32 * 4)(*[(k >> (32 * i)) & 0xFFFFFFFF for i in range(4)])
+        assert hc.hc_g1_mul_u128_cmp(p, k4) == 1, hex(k)
+
+
 def test_g2d_add_special_cases(hc):
     """k_combine_sigs' digit-tower G2 addition (g2d.hpp g2d_add) equals curve.hpp g2_add on general
     Jacobian operands and on every special case (equal, opposite, identity operands), decided by

@@ -386,6 +386,15 @@ int hc_g2_mul_u64_cmp(const uint8_t* q96, uint64_t k) {
   if (a.inf || b.inf || c.inf) return a.inf == b.inf && b.inf == c.inf ? 1 : 0;
   return fq2_eq(a.x, b.x) && fq2_eq(a.y, b.y) && fq2_eq(a.x, c.x) && fq2_eq(a.y, c.y) ? 1 : 0;
 }
+// the threshold combine's 128-bit G1 window multiplication: digit tower (g1d.hpp) against the
+// 12-limb curve.hpp g1_mul_u128_w4 (k4: four little-endian words)
+int hc_g1_mul_u128_cmp(const uint8_t* p48, const uint32_t* k4) {
+  g1a P;
+  if (g1_decompress(p48, P) != HBX_PT_OK) return -1;
+  const g1a a = g1_to_affine(g1_mul_u128_w4(P, k4)), b = g1_to_affine(g1d_mul_u128_w4(P, k4));
+  if (a.inf || b.inf) return a.inf == b.inf ? 1 : 0;
+  return fq_eq(a.x, b.x) && fq_eq(a.y, b.y) ? 1 : 0;
+}
 // g2d_add (digit tower, exact special cases) against g2_add over the cases the combine's lane tree
 // can meet: P + Q, P + P, P + (-P), O + P, P + O, O + O, with the operands' Z scaled by z0
 // (Jacobian inputs, not only Z = 1).  Returns a bit mask of the cases that agree (63 = all).
