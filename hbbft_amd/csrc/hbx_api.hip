@@ -679,9 +679,11 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     timed t_(c, HBX_K_PREPARE_LINES, s);
     const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
     const bool own_entry = m_early && me_early != UINT32_MAX;
-    // grouped addition steps (g2_raw_lines_group) only when the epoch's one-lane share checks would
-    // not fill the chip -- the fill test the check launch uses: their larger register footprint
-    // slowed two full N=256 epochs in flight 28.2 -> 32.5 ms per epoch (profiles/r03n_bisect_*)
+    // grouped addition steps (g2_raw_lines_group<true>) only when the epoch's one-lane share checks
+    // would not fill the chip -- the fill test the check launch uses.  At N=256 the grouped kernel
+    // is the faster one alone (lines 1.00 -> 0.85 ms since the group rounds pick their operands by
+    // blocks, epoch 23.38 -> 23.30 ms) but two epochs in flight went 22.7 -> 23.4 ms per epoch: its
+    // register footprint slows the other epoch's checks (round 3: 28.2 -> 32.5, r03n_bisect_*).
     const size_t senders = early_n ? early_n : c->n_keys;
     const bool grouped = senders ? ((size_t)p * senders + 63) / 64 < (size_t)VERIFY_FILL_WAVES : p <= 64;
     auto kpl = grouped ? k_prepare_lines<true> : k_prepare_lines<false>;
@@ -1378,7 +1380,7 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
   if (lanes == 1 && !c->coin_lines_ready) {
     // H''s prepared lines for the one-lane kernel (wave-uniform loads)
     timed t_(c, HBX_K_PREPARE_LINES, s);
-    hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
+    hipLaunchKernelGGL(k_prepare_lines<true>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
                        c->coin_lines_d.as<line_pre_d>(), c->coin_scratch.as<fq2d>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                        UINT32_MAX, nullptr, nullptr, nullptr);
     HIPCHK(c, hipGetLastError());
@@ -1506,7 +1508,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
   hipLaunchKernelGGL(k_decompress_g2, dim3((count + 63) / 64), dim3(64), 0, s, c->vs_sig96.as<uint8_t>(), (size_t)count,
                      c->vs_sig.as<g2a>(), c->vs_sig_st.as<int32_t>(), 1u);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_prepare_lines<false>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
+  hipLaunchKernelGGL(k_prepare_lines<true>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->vs_H.as<g2a>(), count,
                      c->vs_lines_d.as<line_pre_d>(), c->vs_scratch.as<fq2d>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
                      UINT32_MAX, nullptr, nullptr, nullptr);
   HIPCHK(c, hipGetLastError());
