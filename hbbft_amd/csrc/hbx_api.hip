@@ -679,14 +679,13 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
     timed t_(c, HBX_K_PREPARE_LINES, s);
     const uint32_t line_blocks = (2 * p * LINE_K + 63) / 64, own_blocks = own ? (p + 63) / 64 : 0;
     const bool own_entry = m_early && me_early != UINT32_MAX;
-    // grouped addition steps (g2_raw_lines_group<true>) only when the epoch's one-lane share checks
-    // would not fill the chip -- the fill test the check launch uses.  At N=256 the grouped kernel
-    // is the faster one alone (lines 1.00 -> 0.85 ms since the group rounds pick their operands by
-    // blocks, epoch 23.38 -> 23.30 ms) but two epochs in flight went 22.7 -> 23.4 ms per epoch: its
-    // register footprint slows the other epoch's checks (round 3: 28.2 -> 32.5, r03n_bisect_*).
-    const size_t senders = early_n ? early_n : c->n_keys;
-    const bool grouped = senders ? ((size_t)p * senders + 63) / 64 < (size_t)VERIFY_FILL_WAVES : p <= 64;
-    auto kpl = grouped ? k_prepare_lines<true> : k_prepare_lines<false>;
+    // grouped addition steps (g2_raw_lines_group<true>) at every size: since the group rounds pick
+    // their operands by blocks (groupd.hpp gd_round) the grouped kernel is the faster one at N=256
+    // too (lines 1.00 -> 0.85 ms, epoch 23.43 -> 23.27 ms averaged over two runs each), and two
+    // epochs in flight stay within the runs' spread (22.7-23.4 ms per epoch either way).  Round 3
+    // had kept it to launches below a full chip: its register footprint then slowed two epochs in
+    // flight 28.2 -> 32.5 ms per epoch (profiles/r03n_bisect_*).
+    auto kpl = k_prepare_lines<true>;
     hipLaunchKernelGGL(kpl, dim3(line_blocks + own_blocks), b64, 0, s, c->G2pts.as<g2a>(), 2 * p,
                        c->lines_d.as<line_pre_d>(), c->scratch.as<fq2d>(), c->dec_st.as<int32_t>(), p,
                        c->ct_ok.as<uint8_t>(), own ? c->own_part.as<g1j>() : nullptr,
