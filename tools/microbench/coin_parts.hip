@@ -55,7 +55,8 @@ __global__ void __launch_bounds__(64) k_coin2(uint32_t* out, uint32_t* gslot) {
   HBX_SEQ();
   op_mul(B, A, false, false, l1);
   HBX_SEQ();
-  const bool v = final_exp2d_is_one(A, B, G1, G2, l1);
+  bool dg = false;  // Granger-Scott squarings only (the shipped kernel compresses with a retry path)
+  const bool v = final_exp2d_is_one<false>(A, B, G1, G2, l1, dg);
   out[s] = v ? 1u : 0u;
 }
 

@@ -7,45 +7,9 @@
 #include "../../hbbft_amd/csrc/hash.hpp"
 #include "../../hbbft_amd/csrc/g2d.hpp"
 using namespace hbx;
+// fqd_relax (fieldd.hpp), fqd_from_row / fqd_sel8 / rows_* (groupd.hpp): the helpers this
+// prototype introduced, now in the headers
 
-__device__ __forceinline__ fqd fqd_relax(const fqd& a) {
-  fqd r;
-  r.d[0] = a.d[0] & DMASK;
-  HBX_LAUNDER(r.d[0]);
-#pragma unroll
-  for (int i = 1; i < 13; i++) {
-    r.d[i] = (a.d[i] & DMASK) + (a.d[i - 1] >> 28);
-    HBX_LAUNDER(r.d[i]);
-  }
-  r.d[13] = a.d[13] + (a.d[12] >> 28);
-  return r;
-}
-__device__ __forceinline__ fq2d fq2d_relax(const fq2d& a) { return fq2d{fqd_relax(a.c0), fqd_relax(a.c1)}; }
-template <int K>
-__device__ __forceinline__ fqd fqd_from_row(const fqd& v) {
-  dpp_guard_src<16, K>();
-  fqd r;
-#pragma unroll
-  for (int i = 0; i < 14; i++) r.d[i] = __builtin_amdgcn_update_dpp(0, v.d[i], 0x150 + K, 0xf, 0xf, false);
-  return r;
-}
-__device__ __forceinline__ fqd fqd_sel8(int s, const fqd& v0, const fqd& v1, const fqd& v2, const fqd& v3, const fqd& v4,
-                                        const fqd& v5, const fqd& v6, const fqd& v7) {
-  fqd r;
-#pragma unroll
-  for (int i = 0; i < 14; i++) {
-    const int32_t lo = (s & 2) ? ((s & 1) ? v3.d[i] : v2.d[i]) : ((s & 1) ? v1.d[i] : v0.d[i]);
-    const int32_t hi = (s & 2) ? ((s & 1) ? v7.d[i] : v6.d[i]) : ((s & 1) ? v5.d[i] : v4.d[i]);
-    r.d[i] = (s & 4) ? hi : lo;
-  }
-  return r;
-}
-template <int K>
-__device__ __forceinline__ fq2d rows_sqr(const fqd& r) { return fq2d{fqd_from_row<K>(r), fqd_dbl(fqd_from_row<K + 1>(r))}; }
-template <int K>
-__device__ __forceinline__ fq2d rows_mul(const fqd& r) {
-  return fq2d{fqd_sub(fqd_from_row<K>(r), fqd_from_row<K + 1>(r)), fqd_add(fqd_from_row<K + 2>(r), fqd_from_row<K + 3>(r))};
-}
 // inputs: relaxed digits (< 2^28 + 8), values < 2^386; outputs the same
 __device__ __forceinline__ g2jd g2d_dbl_group_r(const g2jd& p, int gl) {
   const int s = gl & 7;
