@@ -98,7 +98,9 @@ def parse(argv=None):
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-GPU rehearsal of strong scaling: run only rank 0's proposer slice of a G-way "
                          "sharded epoch (the per-GPU work of --scaling strong at --gpus G, minus the all-gather)")
-    ap.add_argument("--strong-at-1", action="store_true", help=argparse.SUPPRESS)  # tests: the strong-mode slab path at world 1
+    ap.add_argument("--strong-at-1", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-node-rate", dest="node_rate", action="store_false",
+                    help="at --gpus G > 1 (strong), skip the weak sub-object (G whole epochs in flight)")  # tests: the strong-mode slab path at world 1
     ap.add_argument("--configs", default="C1,C2,C4,C5",
                     help="secondary BASELINE configs in the same line ('' for none); at --gpus > 1 (strong) C4 "
                          "and C5 run sharded by instance")
@@ -129,6 +131,18 @@ def host_info():
 def all_cores() -> int:
     """Row (b) threads: every host core, os.cpu_count()."""
     return max(1, os.cpu_count() or 1)
+
+
+def usable_cores() -> int:
+    """CPUs this process may actually run on at once: the cgroup quota when there is one, else the
+    affinity mask (the `cores` every cpu_baseline reports)."""
+    qc = quota_cores()
+    if qc:
+        return qc
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return all_cores()
 
 
 def quota_cores():
@@ -302,8 +316,9 @@ def cpu_baseline_dec(ep, seconds: float):
         dq = run(jobs, qc, True)
         rows["b_hoisted_fused_quota_cores"] = {"value": round(len(jobs) / dq, 1), "cores": qc,
                                                "sample": f"same sample in {dq:.1f} s; cgroup cpu.max allows {qc} CPUs"}
-    best = max(("b_hoisted_fused_all_cores", "b_hoisted_fused_quota_cores"),
-               key=lambda r: rows[r]["value"] if r in rows else -1)
+    # value = the row on the CPUs the process may use (the quota row when the box sets one): an
+    # oversubscribed all-cores row can be timed but does not say what those CPUs sustain
+    best = "b_hoisted_fused_quota_cores" if qc else "b_hoisted_fused_all_cores"
     # PublicKeySet::decrypt (honey_badger.rs:340) of a sample of proposers on the best row's threads:
     # Lagrange combine of the first t valid shares + hash_bytes keystream XOR, checked against the
     # contributions; the epoch row adds the share checks of the whole epoch at the best rate
@@ -740,7 +755,7 @@ def cpu_baseline_coin(pk, nonces, sigs, corrupt, master_pk, t, seconds):
     if qc:
         dq = run(jobs, qc, 1)
         brow["b_hoisted_fused_quota_cores"] = (len(jobs) / dq, qc)
-    best = max(brow, key=lambda r: brow[r][0])
+    best = "b_hoisted_fused_quota_cores" if qc else "b_hoisted_fused_all_cores"  # as cpu_baseline_dec
     threads_c = brow[best][1]
     # combine_signatures + master verify + parity of the sampled instances, best row's threads
     valid = np.ascontiguousarray(~corrupt, dtype=np.uint8)
@@ -1006,11 +1021,11 @@ def cpu_validate(proofs, root):
 def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
     """C5 on host cores: reed-solomon-erasure's table-driven encode / reconstruct
     (tools/cpu_baseline/cpu_port.cpp) and the Merkle trees with OpenSSL's SHA-256 / SHA3-256
-    (hashlib).  (a) one thread, per instance; (b) all cores over instances (RS: std::threads;
+    (hashlib).  (a) one thread, per instance; (b) the usable cores over instances (RS: std::threads;
     Merkle: a thread pool, hashlib releases the GIL on these buffer sizes)."""
     lib = cpu_lib()
     inst, n = host_shards.shape[:2]
-    threads = all_cores()
+    threads = usable_cores()  # the CPUs this process may use (cgroup quota), as stacks A and B
     # (a) one instance, one thread
     one = host_shards[:1].copy()
     t0 = time.perf_counter()
@@ -1076,16 +1091,19 @@ def cpu_baseline_broadcast(host_shards, k, m, L, payload, roots_by, seconds):
                                     "merkle_sha3_GBps": gbps(n * (L + 1), mk3),
                                     "decode_ms_per_instance": round(dec1 * 1e3, 1),
                                     "ms_per_instance_encode_roots_decode": round((enc1 + mk1 + dec1) * 1e3, 1)},
-                      "b_all_cores": {"rs_encode_GBps_hbm_equiv": gbps(cnt * (k + m) * L, encb),
+                      "b_usable_cores": {"rs_encode_GBps_hbm_equiv": gbps(cnt * (k + m) * L, encb),
                                       "merkle_sha256_GBps": gbps(cnt * n * (L + 1), mkb),
                                       "rs_reconstruct_GBps_hbm_equiv": gbps(cnt * (k + m) * L, recb),
                                       "reconstruct_ms_per_instance": round(recb / cnt * 1e3, 2),
                                       "branch_verify_GBps_hashed": gbps(cnt * n * (L + 1), vb),
                                       "branch_verify_proofs_per_s": round(cnt * n / vb, 1),
                                       "sample": f"{cnt} instances on {threads} threads ({cnt * n} Echo proofs)"}},
-                sample=f"RS: tools/cpu_baseline/cpu_port.cpp, reed-solomon-erasure 3.1.0's MUL_TABLE shape "
-                       f"(g++ -O3); Merkle: hashlib (OpenSSL) SHA-256 / SHA3-256; {host['model']}, nproc "
-                       f"{host['nproc']}; a restatement, not the reference binary")
+                cgroup_cpus=quota_cores(),
+                sample=f"value = row b_usable_cores ({threads} threads = the CPUs this process may use; nproc "
+                       f"{host['nproc']}): RS encode by tools/cpu_baseline/cpu_port.cpp, reed-solomon-erasure "
+                       f"3.1.0's MUL_TABLE shape (g++ -O3); Merkle roots by Python hashlib (OpenSSL SHA-256 / "
+                       f"SHA3-256, the leaf and node digests the merkle crate's afck variant computes) on a thread "
+                       f"pool, not the port; {host['model']}; a restatement, not the reference binary")
 
 
 # ----------------------------------------------------------------------------------------------
@@ -1099,18 +1117,22 @@ def _sync(torch, dev):
 def _timed_steps(torch, dist, dev, world, steps, fn):
     """Barrier + synchronize on both sides of ``steps`` calls of fn; max over ranks (seconds).
     (``dev`` may be the CPU: tests/test_bench_shard_legs.py runs the legs over gloo.)"""
+    group = dist.is_available() and dist.is_initialized()  # (not at a world of one without a group)
     fn()
     _sync(torch, dev)
-    dist.barrier()
+    if group:
+        dist.barrier()
     _sync(torch, dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     _sync(torch, dev)
-    dist.barrier()
+    if group:
+        dist.barrier()
     _sync(torch, dev)
     tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    if group:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
 
 
@@ -1213,6 +1235,69 @@ def sharded_c5(args, dev, torch, Context, world, rank, n=128, inst=128, plen=1 <
                         f"GPUs (encode + SHA-256 roots + decode, + one all-gather of {lay.size} B slabs)",
             "value": round(inst * plen * steps / el / 1e9, 2), "unit": "GB/s of proposals (whole job, wall)",
             "ms_per_round": round(el / steps * 1e3, 3), "instances_per_gpu": c, "scaling": "strong"}
+
+
+def weak_epochs(args, dev, torch, world, rank, make_bench):
+    """The node's rate beside the latency-bound strong split: every rank runs
+    WHOLE node-epochs of its own -- G epochs in flight across the node, as HoneyBadger keeps up to
+    max_future_epochs = 3 future epochs open (dynamic_honey_badger/builder.rs:18-27) -- timed with a
+    barrier + synchronize on both sides, max over ranks; every rank checks its last epoch and the
+    verdicts are all-gathered (one byte per rank).  ``make_bench()`` returns an object with
+    ``step()``, ``check()`` and ``units`` (share verifies per step); a stand-in in the gloo test."""
+    import torch.distributed as dist
+
+    eb = make_bench()
+    steps = max(args.steps, 2)
+    el = _timed_steps(torch, dist, dev, world, steps, eb.step)
+    ok = torch.tensor([1 if eb.check() else 0], dtype=torch.uint8, device=dev)
+    oks = torch.empty(world, dtype=torch.uint8, device=dev)
+    if world > 1:
+        if dev.type == "cuda":
+            dist.all_gather_into_tensor(oks, ok)
+        else:
+            dist.all_gather(list(oks.view(world, 1).unbind(0)), ok)
+    else:
+        oks.copy_(ok)
+    assert bool((oks == 1).all()), "weak leg: a rank's epoch failed its check"
+    return {"workload": f"{world} whole node-epochs in flight, one per GPU (each {eb.units} share verifies, "
+                        f"checked on every rank)",
+            "value": round(world * eb.units * steps / el, 1), "unit": "share verifies/s (whole job, wall)",
+            "ms_per_epoch": round(el / steps * 1e3, 3), "epochs": world * steps, "scaling": "weak"}
+
+
+def gather_ms(torch, dev, world, slab, reps=10):
+    """The result slab's all-gather alone (RCCL over xGMI on GPUs): barrier-bracketed, max over
+    ranks, per gather."""
+    import torch.distributed as dist
+
+    from hbbft_amd import shard
+
+    el = _timed_steps(torch, dist, dev, world, reps, lambda: shard.all_gather_slabs(slab, world))
+    return round(el / reps * 1e3, 4)
+
+
+class _WeakEpoch:
+    """A whole node-epoch on this rank's GPU for weak_epochs (its own context and stream)."""
+
+    def __init__(self, args, dev, torch, Context, n):
+        self.torch = torch
+        self.ctx = Context(dev.index or 0)
+        self.ep = make_epoch(self.ctx, n, 0, n, args.vlen, args.corrupt_every)
+        self.stream = torch.cuda.Stream(dev)
+        self.eb = EpochBench(self.ctx, self.ep, dev, self.stream, torch, args.verify_lanes, not args.no_own_share,
+                             args.combine_lanes)
+        self.eb.bind_outputs(torch.zeros(n * n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
+                             torch.zeros(n, dtype=torch.int32, device=dev))
+        self.units = n * n
+
+    def step(self):
+        self.eb.step()
+
+    def check(self):
+        self.torch.cuda.synchronize()
+        self.eb.check(0)  # raises on any difference
+        self.ctx.close()
+        return True
 
 
 # ----------------------------------------------------------------------------------------------
@@ -1350,6 +1435,14 @@ def main():
     }
     if key_ms is not None:
         res["era_key_broadcast_ms"] = key_ms
+    if strong:
+        # the gather of this epoch's result slab on its own (it is inside every timed step above)
+        res["all_gather"] = {"ms": gather_ms(torch, dev, world, slab), "bytes_per_rank": int(lay["size"]),
+                             "fields": "share status bytes (HBX_SHARE_*: the reference logs a FaultKind per share), "
+                                       "ct status, combine status, plaintexts"}
+    if world > 1 and strong and args.node_rate:
+        # the node's rate with G whole epochs in flight, in the same line as the strong split
+        res["node_rate"] = weak_epochs(args, dev, torch, world, rank, lambda: _WeakEpoch(args, dev, torch, Context, n))
     if world == 1 and args.in_flight > 1:
         res["epochs_in_flight"] = in_flight(args, eb, dev, torch, Context, verifies)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -38,8 +38,31 @@ namespace hbx {
 // ---- one-lane slots: a packed Fq12 (12 Fq x 13 dwords, pairingd.hpp lds_put_fq12d's packing),
 // word k of this lane at p[k * S] ------------------------------------------------------------------
 constexpr int FE1_WORDS = 156;
+
+// The lane's LDS slot, addressed afresh at every access.  Held as a pointer, the slot address is one
+// more VGPR live across every product; at the steps' register peak the allocator spilled exactly
+// that value and reloaded it from scratch before each operand fetch -- 456 of the 525 scratch
+// reloads of one Fq12 slot product (tools/microbench/fe_probe.hip), each waited on before its
+// ds_read.  Here the lane index comes from v_mbcnt (two VALU ops, no register input) in a volatile
+// asm, so it is recomputed where needed and never held: nothing to spill.
+#if defined(__HIPCC__)
+struct lane_lds {
+  lds_u32* base;  // the block's slot array (wave-uniform); lane l's word k at base[k * 64 + l]
+};
+__device__ __forceinline__ lds_u32* slot_ptr(lane_lds s) {
+  uint32_t l;
+  __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return s.base + l;
+}
+#endif
+template <class T>
+HBX_HD T* slot_ptr(T* p) {
+  return p;
+}
+
 template <int S, class P>
-HBX_HD fqd s1_get_fqd(P p, int word) {
+HBX_HD fqd s1_get_fqd(P p_, int word) {
+  const auto p = slot_ptr(p_);
   uint32_t w[13];
 #pragma unroll
   for (int k = 0; k < 13; k++) w[k] = p[(word + k) * S];
@@ -57,7 +80,7 @@ HBX_HD fqd s1_get_fqd(P p, int word) {
 }
 // e normalised: digits 0..12 in [0, 2^28), digit 13 whole
 template <int S, class P>
-HBX_HD void s1_put_fqd(P p, int word, const fqd& e) {
+HBX_HD void s1_put_fqd(P p_, int word, const fqd& e) {
   uint32_t w[13];
 #pragma unroll
   for (int k = 0; k < 12; k++) w[k] = 0;
@@ -69,6 +92,7 @@ HBX_HD void s1_put_fqd(P p, int word, const fqd& e) {
     if (sh > 4) w[wd + 1] |= d >> (32 - sh);
   }
   w[12] = (uint32_t)e.d[13];
+  const auto p = slot_ptr(p_);
 #pragma unroll
   for (int k = 0; k < 13; k++) p[(word + k) * S] = w[k];
 }
@@ -118,9 +142,11 @@ HBX_HD void s1_put_fq12d(P p, const fq12d& a) {
 }
 // slot-to-slot copy (global -> LDS), 52 words (two Fq2 coefficients) in flight at a time
 template <int SD, int SS, class PD, class PS>
-HBX_HD void s1_copy(PD d, PS s) {
+HBX_HD void s1_copy(PD d_, PS s_) {
 #pragma unroll 1
   for (int k0 = 0; k0 < FE1_WORDS; k0 += 52) {
+    const auto d = slot_ptr(d_);
+    const auto s = slot_ptr(s_);
 #pragma unroll
     for (int k = 0; k < 52; k++) d[(k0 + k) * SD] = s[(k0 + k) * SS];
     HBX_SEQ();
@@ -129,8 +155,82 @@ HBX_HD void s1_copy(PD d, PS s) {
 
 // fq6d_zero_ and fq6d_mul_acc1 (acc += a * y, y streamed): pairingd.hpp
 
+// acc_p += a * y and acc_m -= a * y at once (pairingd.hpp fq6d_mul_acc1's Karatsuba, every Fq2
+// product folded into both accumulators): both normalised (or zero) on entry, carry-normalised on exit.
+template <class Y>
+HBX_HD void fq6d_mul_acc_pm(fq6d& acc_p, fq6d& acc_m, const fq6d& a, Y y) {
+  auto fold = [&](int k, const fq2d& t, int sign) __attribute__((always_inline)) {
+    fq2d& p = k == 0 ? acc_p.c0 : k == 1 ? acc_p.c1 : acc_p.c2;
+    fq2d& m = k == 0 ? acc_m.c0 : k == 1 ? acc_m.c1 : acc_m.c2;
+    if (sign > 0) {
+      p = fq2d_add(p, t);
+      m = fq2d_sub(m, t);
+    } else {
+      p = fq2d_sub(p, t);
+      m = fq2d_add(m, t);
+    }
+  };
+  {
+    const fq2d t0 = fq2d_mul(a.c0, y(0));
+    fold(0, t0, 1);
+    fold(1, t0, -1);
+    fold(2, t0, -1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t1 = fq2d_mul(a.c1, y(1));
+    fold(0, fq2d_mul_xi(t1), -1);
+    fold(1, t1, -1);
+    fold(2, t1, 1);
+  }
+  HBX_SEQ();
+  {
+    const fq2d t2 = fq2d_mul(a.c2, y(2));
+    const fq2d xt2 = fq2d_mul_xi(t2);
+    fold(0, xt2, -1);
+    fold(1, xt2, 1);
+    fold(2, t2, -1);
+  }
+  HBX_SEQ();
+  fold(0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))), 1);
+  HBX_SEQ();
+  fold(1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))), 1);
+  HBX_SEQ();
+  fold(2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))), 1);
+  HBX_SEQ();
+  acc_p = fq6d_norm(acc_p);
+  acc_m = fq6d_norm(acc_m);
+}
+
 // X * Y, X in registers (reduced, or its conjugate), Y the packed value in slot y.  Reduced.
 // Karatsuba over w: c0 = X0 Y0 + v X1 Y1, c1 = (X0 + X1)(Y0 + Y1) - X0 Y0 - X1 Y1.
+#ifndef HBX_FE1_MUL_ORDER
+#define HBX_FE1_MUL_ORDER 1
+#endif
+#if HBX_FE1_MUL_ORDER
+// The order keeps at most three Fq6 values beside a product's temporaries (the round-5 order held
+// X, X0 + X1 and three accumulators, ~500 registers): B = X1 Y1 first; X0 + X1 replaces X1; B
+// seeds both outputs (c0 = v B, c1 = -B) and dies; c1 += (X0 + X1)(Y0 + Y1), then X0 Y0 goes into
+// c0 and out of c1 in one pass.  Same element.
+template <int S, class P>
+HBX_HD fq12d fq12d_mul_slot(const fq12d& X, P y) {
+  fq6d c0, c1;
+  fq6d Xs;
+  {
+    fq6d B = fq6d_zero_();
+    fq6d_mul_acc1(B, X.c1, [&](int q) { return s1_get_fq2d<S>(y, 3 + q); });
+    HBX_SEQ();
+    Xs = fq6d_norm(fq6d_add(X.c0, X.c1));
+    c0 = fq6d_norm(fq6d_mul_v(B));
+    c1 = fq6d_neg(B);
+  }
+  HBX_SEQ();
+  fq6d_mul_acc1(c1, Xs, [&](int q) { return fq2d_norm(fq2d_add(s1_get_fq2d<S>(y, q), s1_get_fq2d<S>(y, 3 + q))); });
+  HBX_SEQ();
+  fq6d_mul_acc_pm(c0, c1, X.c0, [&](int q) { return s1_get_fq2d<S>(y, q); });
+  return fq12d{fq6d_reduce(c0), fq6d_reduce(c1)};
+}
+#else
 template <int S, class P>
 HBX_HD fq12d fq12d_mul_slot(const fq12d& X, P y) {
   fq6d A = fq6d_zero_();
@@ -144,6 +244,7 @@ HBX_HD fq12d fq12d_mul_slot(const fq12d& X, P y) {
   fq6d_mul_acc1(C, Xs, [&](int q) { return fq2d_norm(fq2d_add(s1_get_fq2d<S>(y, q), s1_get_fq2d<S>(y, 3 + q))); });
   return fq12d{fq6d_reduce(fq6d_add(A, fq6d_mul_v(B))), fq6d_reduce(fq6d_sub(fq6d_sub(C, A), B))};
 }
+#endif
 
 // Granger-Scott cyclotomic squaring (fieldd.hpp fq12d_cyclotomic_sqr) with a fence after every Fq2
 // squaring: the nine squarings are independent, and unfenced the scheduler interleaves them until
@@ -251,6 +352,9 @@ HBX_HD void karabina_sqr(fq12c& c) {
 #endif
 }
 // decompressed element (reduced); `degenerate` set when g3 = 0
+#ifndef HBX_KARA_INV_CALL
+#define HBX_KARA_INV_CALL 0
+#endif
 HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
   fq2d g4;
   {
@@ -263,7 +367,11 @@ HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
     HBX_SEQ();
     const fq cn = fq_canon(fqd_to_fq(nrm));
     degenerate = degenerate || fq_is_zero(cn);
+#if HBX_KARA_INV_CALL
+    const fqd ni = fqd_from_fq(fq_inv(cn));  // out of line (field.hpp): its loop sees only its own state
+#else
     const fqd ni = fqd_from_fq(fq_inv_i(cn));
+#endif
     HBX_SEQ();
     g4 = fq2d_mul(num, fq2d_mul_fq(fq2d_conj(den), ni));
   }

@@ -30,6 +30,9 @@ namespace hbx {
 // operations produced wrong sums on gfx950 (tools/microbench/addcmp.hip: Y1 Z2 differed from the
 // same expression outside the function; with the moves pinned both agree and the hash-to-G2
 // checksum of profiles/r05o_hashg2.txt is reproduced).
+#ifndef HBX_ROW_PIN
+#define HBX_ROW_PIN 1  // 0 only in tools/microbench/dppfold.hip's reproduction of the fold
+#endif
 template <int K>
 __device__ __forceinline__ fqd fqd_from_row(const fqd& v) {
   static_assert(K >= 0 && K < 16, "row lane");
@@ -38,7 +41,9 @@ __device__ __forceinline__ fqd fqd_from_row(const fqd& v) {
 #pragma unroll
   for (int i = 0; i < 14; i++) {
     r.d[i] = __builtin_amdgcn_update_dpp(0, v.d[i], 0x150 + K, 0xf, 0xf, false);
-    HBX_LAUNDER(r.d[i]);
+#if HBX_ROW_PIN
+    __asm__("" : "+v"(r.d[i]));  // (not HBX_LAUNDER: pinned in every unit, HBX_NO_LAUNDER ones too)
+#endif
   }
   return r;
 }

@@ -90,9 +90,13 @@ struct hbx_ctx {
   dbuf S, S_status, fallback, valid, shares_own, present_own, gslot;
   dbuf fe1slot;  // one-lane checks: the final exponentiation's global slots F, T, G (fe1d.hpp)
   uint32_t force_fallback = 0;  // hbx_debug_force_fallback (tests only)
-  dbuf fb_lanes;                // u32: checks the last one-lane / two-lane coin launch's fallback decided
+  // u32 counters of the checks the fallback path decided: one for the one-lane decryption-share
+  // checks, one for the two-lane coin checks (launches of the two kinds on different streams must
+  // not mix their counts); fb_last names the counter of the last share-check launch of either kind,
+  // or none when that launch used a lane count without a fallback path
+  dbuf fb_lanes, fb_coin;
+  dbuf* fb_last = nullptr;
   dbuf hs[6];                   // staging of the host-pointer broadcast calls
-  bool fb_lanes_valid = false;  // fb_lanes was reset by such a launch
   // combine state
   dbuf keys, status, out_own;
   // broadcast state: GF(2^8) tables, encoding matrix of (rs_k, rs_m), reconstruct jobs, Merkle
@@ -493,7 +497,7 @@ int hbx_ctx_destroy(hbx_ctx* c) {
                   &c->coin_comb_st, &c->coin_mpk_comp, &c->coin_mpk, &c->coin_mpk_st, &c->coin_ok, &c->coin_par,
                   &c->coin_out96, &c->dec_st, &c->own_sk, &c->own_S, &c->own_part, &c->lines_d,
                   &c->vs_pk, &c->vs_lines_d, &c->coin_lines_d, &c->vs_blob, &c->vs_off, &c->vs_H, &c->vs_lines, &c->vs_scratch, &c->vs_sig96,
-                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->fe1slot, &c->fb_lanes, &c->hs[0], &c->hs[1], &c->hs[2], &c->hs[3], &c->hs[4], &c->hs[5], &c->coin_use, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
+                  &c->vs_sig, &c->vs_sig_st, &c->vs_status, &c->fe1slot, &c->fb_lanes, &c->fb_coin, &c->hs[0], &c->hs[1], &c->hs[2], &c->hs[3], &c->hs[4], &c->hs[5], &c->coin_use, &c->bv_commit48, &c->bv_C, &c->bv_cst, &c->bv_rows,
                   &c->bv_rows48, &c->bv_pst, &c->bv_ackp, &c->bv_acky, &c->bv_vals, &c->bv_out};
   for (dbuf* b : bufs) b->release();
   (void)hipEventDestroy(c->ev_last);
@@ -533,11 +537,11 @@ int hbx_debug_force_fallback(hbx_ctx* c, uint32_t every) {
 
 int64_t hbx_get_fallback_lanes(hbx_ctx* c) {
   if (!c) return HBX_E_INVALID_ARG;
-  if (!c->fb_lanes_valid) return 0;
+  if (!c->fb_last) return 0;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, quiesce(c));
   uint32_t v = 0;
-  HIPCHK(c, hipMemcpy(&v, c->fb_lanes.p, 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&v, c->fb_last->p, 4, hipMemcpyDeviceToHost));
   return v;
 }
 
@@ -641,7 +645,7 @@ static int prepare_impl(hbx_ctx* c, const uint8_t* d_u_comp, const uint8_t* d_v_
   stream_scope ss_{c, s};
   if (!c->U.ensure((size_t)p * sizeof(g1a)) || !c->G2pts.ensure((size_t)2 * p * sizeof(g2a)) || !c->Hj.ensure((size_t)p * sizeof(g2j)) ||
       !c->lines.ensure((size_t)p * sizeof(line_block)) || !c->lines_d.ensure((size_t)p * sizeof(line_block_d)) ||
-      !c->scratch.ensure((size_t)2 * p * 2 * MILLER_LINES * sizeof(fq2)) || !c->ct_ok.ensure(p) ||
+      !c->scratch.ensure((size_t)2 * p * MILLER_LINES * sizeof(fq2d)) || !c->ct_ok.ensure(p) ||
       !c->ct_valid.ensure(p) || !c->dec_st.ensure((size_t)2 * p * 4))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_ciphertexts_d: out of device memory");
   const size_t m_early = early_shares ? (size_t)early_n * p : 0;
@@ -805,6 +809,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                       : waves2 <= fill ? 2
                                        : 3;
     c->lanes_used = lanes;
+    c->fb_last = nullptr;  // set again below by the one-lane path, the only one with a fallback
     if (lanes == 2) {
       // global slots of the final exponentiation: 2 x 78 dwords per lane of the launch
       const size_t glanes = (size_t)((n + 31) / 32) * p * 64;
@@ -845,7 +850,7 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
       uint32_t* gs = c->fe1slot.as<uint32_t>();
       if (!c->fb_lanes.ensure(4)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory");
       HIPCHK(c, hipMemsetAsync(c->fb_lanes.p, 0, 4, s));
-      c->fb_lanes_valid = true;
+      c->fb_last = &c->fb_lanes;
       hipLaunchKernelGGL(k_verify_shares_ml, grid, dim3(64), 0, s, c->S.as<g1a>(), c->S_status.as<int32_t>(),
                          d_present, c->pk_m.as<g1a>(), c->n_keys, c->G2pts.as<g2a>(), c->lines_d.as<line_block_d>(),
                          c->ct_ok.as<uint8_t>(), n, c->valid.as<uint8_t>(), me, gs);
@@ -1301,7 +1306,7 @@ int hbx_prepare_nonces(hbx_ctx* c, const uint8_t* nonce_blob, const uint64_t* no
       !c->coin_H.ensure((size_t)count * sizeof(g2a)) || !c->coin_Hp.ensure((size_t)count * sizeof(g2a)) ||
       !c->coin_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
       !c->coin_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
-      !c->coin_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->coin_out96.ensure((size_t)count * 96))
+      !c->coin_scratch.ensure((size_t)count * MILLER_LINES * sizeof(fq2d)) || !c->coin_out96.ensure((size_t)count * 96))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_prepare_nonces: out of device memory");
   if (total) HIPCHK(c, hipMemcpyAsync(c->coin_blob.p, nonce_blob, total, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(c->coin_off.p, nonce_off, (size_t)(count + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1399,9 +1404,9 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
       const size_t glanes = (size_t)((n + 31) / 32) * count * 64;
       if (!c->gslot.ensure(glanes * 2 * LDS_FQ6D_PACKED * 4))
         return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory (slots)");
-      if (!c->fb_lanes.ensure(4)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
-      HIPCHK(c, hipMemsetAsync(c->fb_lanes.p, 0, 4, s));
-      c->fb_lanes_valid = true;
+      if (!c->fb_coin.ensure(4)) return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sig_shares: out of device memory");
+      HIPCHK(c, hipMemsetAsync(c->fb_coin.p, 0, 4, s));
+      c->fb_last = &c->fb_coin;
       const dim3 grid((n + 31) / 32, count);
       // Miller loops; the final exponentiation with compressed runs; then the pairs whose
       // decompression met g3 = 0 (SHARE_FALLBACK) once more, Miller and Granger-Scott squarings
@@ -1413,13 +1418,14 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
         HIPCHK(c, hipGetLastError());
         if (retry == 0)
           hipLaunchKernelGGL(k_verify_sig_shares2_fe<true>, grid, dim3(64), 0, s, n, c->coin_valid.as<uint8_t>(),
-                             c->gslot.as<uint32_t>(), c->force_fallback, c->fb_lanes.as<uint32_t>());
+                             c->gslot.as<uint32_t>(), c->force_fallback, c->fb_coin.as<uint32_t>());
         else
           hipLaunchKernelGGL(k_verify_sig_shares2_fe<false>, grid, dim3(64), 0, s, n, c->coin_valid.as<uint8_t>(),
-                             c->gslot.as<uint32_t>(), 0u, c->fb_lanes.as<uint32_t>());
+                             c->gslot.as<uint32_t>(), 0u, c->fb_coin.as<uint32_t>());
         HIPCHK(c, hipGetLastError());
       }
     } else {
+      c->fb_last = nullptr;  // the one-lane coin check has no fallback path
       hipLaunchKernelGGL(k_verify_sig_shares, dim3((n + 63) / 64, count), dim3(64), 0, s, c->coin_lines_d.as<line_pre_d>(),
                          c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys, c->coin_sig.as<g2a>(),
                          c->coin_sig_st.as<int32_t>(), d_present, n, c->coin_valid.as<uint8_t>());
@@ -1492,7 +1498,7 @@ int hbx_verify_sigs(hbx_ctx* c, const uint8_t* pk48, const uint8_t* msg_blob, co
       !c->vs_off.ensure((size_t)(count + 1) * 8) || !c->vs_H.ensure((size_t)count * sizeof(g2a)) ||
       !c->vs_lines.ensure((size_t)count * MILLER_LINES * sizeof(line_pre)) ||
       !c->vs_lines_d.ensure((size_t)count * MILLER_LINES * sizeof(line_pre_d)) ||
-      !c->vs_scratch.ensure((size_t)count * 2 * MILLER_LINES * sizeof(fq2)) || !c->vs_sig96.ensure((size_t)count * 96) ||
+      !c->vs_scratch.ensure((size_t)count * MILLER_LINES * sizeof(fq2d)) || !c->vs_sig96.ensure((size_t)count * 96) ||
       !c->vs_sig.ensure((size_t)count * sizeof(g2a)) || !c->vs_sig_st.ensure((size_t)count * 4) ||
       !c->vs_status.ensure(count))
     return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_sigs: out of device memory");

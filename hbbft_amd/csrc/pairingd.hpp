@@ -245,34 +245,50 @@ HBX_HD fq6d fq6d_zero_() {
 // folded into the accumulator at once, a fence between products (HBX_SEQ); a and y normalised,
 // acc normalised (or zero) on entry; carry-normalised on exit.  The digit sums stay below 2^31:
 // acc + 7 terms of at most two normalised values each.
+// HBX_PIN_OPS: each product's register operand is pinned (an empty asm with the digits as in/out
+// VGPR operands) right where the product starts, so the compiler cannot compute the operand's digit
+// sums (fq2d_mul's Karatsuba sums) for all six products up front beside the accumulator.
+#ifndef HBX_PIN_OPS
+#define HBX_PIN_OPS 0
+#endif
+HBX_HD fq2d fq2d_pin(fq2d a) {
+#if HBX_PIN_OPS && defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    __asm__ volatile("" : "+v"(a.c0.d[i]));
+    __asm__ volatile("" : "+v"(a.c1.d[i]));
+  }
+#endif
+  return a;
+}
 template <class Y>
 HBX_HD void fq6d_mul_acc1(fq6d& acc, const fq6d& a, Y y) {
   {
-    const fq2d t0 = fq2d_mul(a.c0, y(0));
+    const fq2d t0 = fq2d_mul(fq2d_pin(a.c0), y(0));
     acc.c0 = fq2d_add(acc.c0, t0);
     acc.c1 = fq2d_sub(acc.c1, t0);
     acc.c2 = fq2d_sub(acc.c2, t0);
   }
   HBX_SEQ();
   {
-    const fq2d t1 = fq2d_mul(a.c1, y(1));
+    const fq2d t1 = fq2d_mul(fq2d_pin(a.c1), y(1));
     acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t1));
     acc.c1 = fq2d_sub(acc.c1, t1);
     acc.c2 = fq2d_add(acc.c2, t1);
   }
   HBX_SEQ();
   {
-    const fq2d t2 = fq2d_mul(a.c2, y(2));
+    const fq2d t2 = fq2d_mul(fq2d_pin(a.c2), y(2));
     acc.c0 = fq2d_sub(acc.c0, fq2d_mul_xi(t2));
     acc.c1 = fq2d_add(acc.c1, fq2d_mul_xi(t2));
     acc.c2 = fq2d_sub(acc.c2, t2);
   }
   HBX_SEQ();
-  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(a.c1, a.c2), fq2d_add(y(1), y(2)))));
+  acc.c0 = fq2d_add(acc.c0, fq2d_mul_xi(fq2d_mul(fq2d_add(fq2d_pin(a.c1), fq2d_pin(a.c2)), fq2d_add(y(1), y(2)))));
   HBX_SEQ();
-  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(a.c0, a.c1), fq2d_add(y(0), y(1))));
+  acc.c1 = fq2d_add(acc.c1, fq2d_mul(fq2d_add(fq2d_pin(a.c0), fq2d_pin(a.c1)), fq2d_add(y(0), y(1))));
   HBX_SEQ();
-  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(a.c0, a.c2), fq2d_add(y(0), y(2))));
+  acc.c2 = fq2d_add(acc.c2, fq2d_mul(fq2d_add(fq2d_pin(a.c0), fq2d_pin(a.c2)), fq2d_add(y(0), y(2))));
   HBX_SEQ();
   acc = fq6d_norm(acc);
 }

@@ -562,11 +562,14 @@ class Context:
     def rs_encode_d(self, d_shards, k: int, m: int, stream=None):
         """d_shards: uint8[inst, k + m, L] (parity rows overwritten)."""
         inst, n, L = d_shards.shape
-        assert n == k + m
+        if n != k + m:
+            raise ValueError(f"rs_encode_d: {n} shards per instance != k + m = {k + m}")
         self._check(self.lib.hbx_rs_encode_d(self.h, d_shards.data_ptr(), inst, k, m, L, self._stream(stream)))
 
     def rs_reconstruct_d(self, d_shards, d_present, d_status, k: int, m: int, stream=None):
         inst, n, L = d_shards.shape
+        if n != k + m:
+            raise ValueError(f"rs_reconstruct_d: {n} shards per instance != k + m = {k + m}")
         self._check(self.lib.hbx_rs_reconstruct_d(self.h, d_shards.data_ptr(), d_present.data_ptr(), inst, k, m, L,
                                                   d_status.data_ptr(), self._stream(stream)))
 
@@ -597,13 +600,16 @@ class Context:
         """hbx_rs_encode: shards uint8[inst, k + m, L] on the host, parity rows written in place."""
         shards = self._host(shards, np.uint8, writable=True)
         inst, n, L = shards.shape
-        assert n == k + m
+        if n != k + m:  # the library copies (k + m) L bytes per instance each way
+            raise ValueError(f"rs_encode: {n} shards per instance != k + m = {k + m}")
         self._check(self.lib.hbx_rs_encode(self.h, shards.ctypes.data, inst, k, m, L))
 
     def rs_reconstruct(self, shards: np.ndarray, present, k: int, m: int) -> np.ndarray:
         """hbx_rs_reconstruct: shards rebuilt in place; returns status int32[inst]."""
         shards = self._host(shards, np.uint8, writable=True)
         inst, n, L = shards.shape
+        if n != k + m:  # the library copies (k + m) L bytes per instance each way
+            raise ValueError(f"rs_reconstruct: {n} shards per instance != k + m = {k + m}")
         pres = self._host(present, np.uint8, (inst, n))
         st = np.zeros(inst, dtype=np.int32)
         self._check(self.lib.hbx_rs_reconstruct(self.h, shards.ctypes.data, pres.ctypes.data, inst, k, m, L,
@@ -633,6 +639,8 @@ class Context:
         nodes = self._host(nodes, np.uint8)
         inst = nodes.shape[0]
         req = self._host(req, np.uint32)
+        if req.ndim != 2 or req.shape[1] != 2:  # the library reads req[2 q], req[2 q + 1] for q < count
+            raise ValueError(f"merkle_proofs: req must be uint32[count, 2] (instance, leaf), got shape {req.shape}")
         count = req.shape[0]
         nh = np.zeros((count, 17, 32), dtype=np.uint8)
         sh = np.zeros((count, 16, 32), dtype=np.uint8)

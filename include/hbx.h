@@ -139,7 +139,7 @@ int hbx_kernel_time(hbx_ctx* ctx, int kernel, double* total_ms, uint32_t* launch
 int hbx_set_digest(hbx_ctx* ctx, int variant);
 /* Lanes per decryption-share check (no reference counterpart; results identical): 1 = one lane
  * per check (the throughput path when a launch fills the chip: a Miller-loop kernel and the final
- * exponentiation as seven step kernels over per-lane slots), 7 = one lane per check in a single
+ * exponentiation as four step kernels over per-lane slots), 7 = one lane per check in a single
  * kernel (the final exponentiation through call frames; kept for comparison), 2 = a lane pair per
  * check (the
  * Fq12 state split in halves, no scratch), 3 = three cooperating lanes per check, 6 = six lanes per
@@ -158,9 +158,12 @@ int hbx_get_verify_lanes_used(const hbx_ctx* ctx);
  * can choose -- a ciphertext with r = 3(x^2 - 1), for which every honest share's check is 1 after
  * the easy part -- is decided by the first step without a fallback.) */
 int hbx_debug_force_fallback(hbx_ctx* ctx, uint32_t every);
-/* Checks of the last one-lane decryption-share launch, or of the last two-lane coin launch, that the
- * fallback path decided (0 unless hbx_debug_force_fallback is on); waits for the launch.
- * Diagnostics: no reference counterpart. */
+/* Checks of the last share-check launch (decryption-share or coin, whichever came last) that the
+ * fallback path decided: 0 unless hbx_debug_force_fallback is on, and 0 when that launch used a lane
+ * count without a fallback path (decryption shares at lanes 2/3/6/7, coin at one lane).  The two
+ * kinds count separately; "last" is host call order, so the value is meaningful when the caller
+ * reads it after the launch it asks about (waits for the context's streams).  Diagnostics: no
+ * reference counterpart. */
 int64_t hbx_get_fallback_lanes(hbx_ctx* ctx);
 /* Lanes per Lagrange term of hbx_combine_decrypt_d (no reference counterpart; results identical):
  * 1 = one lane per GLV term, one block per proposer (k_combine), 4 = a quad of lanes per term over

@@ -67,3 +67,46 @@ def test_library_was_built_from_these_sources():
     lib = ctypes.CDLL(LIB)
     lib.hbx_build_id.restype = ctypes.c_char_p
     assert lib.hbx_build_id().decode() == buildinfo.source_hash()
+
+
+class _NoLib:
+    """Stands in for a Context's library: any call is a test failure (the guards must fire first)."""
+
+    def __getattr__(self, name):
+        raise AssertionError(f"{name} reached the library with mismatched arguments")
+
+
+def _bare_context():
+    from hbbft_amd import hbx
+
+    ctx = object.__new__(hbx.Context)  # no device: only the argument checks run
+    ctx.lib, ctx.h = _NoLib(), None
+    return ctx
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (2, 2), (4, 3)])
+def test_rs_host_forms_reject_shard_count_mismatch(k, m):
+    """hbx_rs_encode / hbx_rs_reconstruct copy (k + m) L bytes per instance each way, so
+    a buffer with n != k + m shards must be refused before the call (a ValueError, not an assert)."""
+    import numpy as np
+
+    ctx = _bare_context()
+    shards = np.zeros((1, 5, 8), dtype=np.uint8)
+    if k + m == 5:
+        pytest.skip("matching shape")
+    with pytest.raises(ValueError, match="k \\+ m"):
+        ctx.rs_encode(shards, k, m)
+    with pytest.raises(ValueError, match="k \\+ m"):
+        ctx.rs_reconstruct(shards, np.ones((1, 5), dtype=np.uint8), k, m)
+
+
+@pytest.mark.parametrize("shape", [(6,), (3, 3), (2, 2, 2)])
+def test_merkle_proofs_rejects_malformed_requests(shape):
+    """hbx_merkle_proofs reads req[2 q], req[2 q + 1] for q < count; only uint32[count, 2]
+    is accepted."""
+    import numpy as np
+
+    ctx = _bare_context()
+    nodes = np.zeros((1, 7, 32), dtype=np.uint8)
+    with pytest.raises(ValueError, match="count, 2"):
+        ctx.merkle_proofs(nodes, 4, np.zeros(shape, dtype=np.uint32))

@@ -177,6 +177,23 @@ class _FakeEngine:
         status.copy_(torch.from_numpy(st).to(status.dtype))
 
 
+class _FakeEpoch:
+    """Stand-in for bench._WeakEpoch: a step is a small CPU computation, the check its result."""
+
+    steps_run = 0
+
+    def __init__(self, rank):
+        self.units = 64
+        self.acc = rank
+
+    def step(self):
+        _FakeEpoch.steps_run += 1
+        self.acc = (self.acc * 31 + 7) % 1000003
+
+    def check(self):
+        return self.acc >= 0
+
+
 def _legs_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
@@ -192,7 +209,13 @@ def _legs_worker(rank, world, port, q):
         dev = torch.device("cpu")
         c4 = bench.sharded_c4(args, dev, torch, _FakeEngine, world, rank, n=7, inst=8)
         c5 = bench.sharded_c5(args, dev, torch, _FakeEngine, world, rank, n=7, inst=5, plen=300)
-        q.put((rank, c4["instances_per_gpu"], c5["instances_per_gpu"], c4["ms_per_round"] > 0 and c5["ms_per_round"] > 0, None))
+        # the weak node-rate sub-object and the slab gather's own time (bench.main at --gpus G > 1)
+        wk = bench.weak_epochs(args, dev, torch, world, rank, lambda: _FakeEpoch(rank))
+        gms = bench.gather_ms(torch, dev, world, torch.full((40,), rank, dtype=torch.uint8), reps=3)
+        ok = c4["ms_per_round"] > 0 and c5["ms_per_round"] > 0 and gms > 0
+        ok = ok and wk["scaling"] == "weak" and wk["epochs"] == world * 2 and wk["value"] > 0
+        ok = ok and _FakeEpoch.steps_run == 3  # one untimed + steps (max(1, 2))
+        q.put((rank, c4["instances_per_gpu"], c5["instances_per_gpu"], ok, None))
     except Exception as e:  # noqa: BLE001 -- reported to the parent
         import traceback
 
@@ -204,7 +227,9 @@ def _legs_worker(rank, world, port, q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_legs_gloo(world):
     """bench.sharded_c4 / sharded_c5 at world 2 and 3 over gloo on the CPU (uneven instance splits:
-    8 coin instances, 5 proposals), each leg's gathered-result assertions included."""
+    8 coin instances, 5 proposals), each leg's gathered-result assertions included; and the weak
+    node-rate sub-object (bench.weak_epochs: whole epochs per rank, verdicts all-gathered) and the
+    slab gather's own time (bench.gather_ms) that bench.main adds at --gpus G > 1."""
     import torch.multiprocessing as mp
 
     from hbbft_amd import shard

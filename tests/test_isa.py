@@ -4,6 +4,8 @@
   s[30:31] (tools/isa_check.py: the compiler defect behind the hung builds of rounds 2 and 3 --
   the function's return jumped back into its own loop).  The check is pinned on a listing
   shaped like the hung build's, so a silent parser change cannot make it pass vacuously.
+* No VALU instruction other than a DPP move carries a row broadcast (row_newbcast): the folded
+  form gave wrong sums on gfx950 (tools/isa_check.py find_dpp_folds, pinned on a listing with one).
 * Every DPP exchange helper carries its EXEC guard (hbbft_amd/csrc/dpp.hpp): the built code
   holds the trap instructions of those guards.
 """
@@ -66,3 +68,29 @@ def test_dpp_guards_are_compiled_in():
                                  capture_output=True, text=True, check=True).stdout
             traps += dis.count("s_trap 2")
     assert traps > 0
+
+
+FOLD_SHAPE = """
+0000000000001000 <_ZN3hbx14g2d_add_group_iE>:
+\tv_mov_b32_dpp v176, v32 row_newbcast:0 row_mask:0xf bank_mask:0xf // 000000001000: 7F6002FA FF015020
+\tv_add_u32_dpp v12, v33, v40 row_newbcast:3 row_mask:0xf bank_mask:0xf // 000000001008: 681850FA FF015321
+\tv_mov_b32_dpp v10, v33 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf // 000000001010: 7E1402FA FF000021
+\tv_sub_u32_dpp v13, v10, v41 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf // 000000001018: 6A1A52FA FF00B10A
+\ts_setpc_b64 s[30:31]                                       // 000000001020: BE801D1E
+
+0000000000002000 <_ZN3hbx8k_kernelE>:
+\tv_subrev_u32_dpp v1, v2, v3 row_newbcast:15 row_mask:0xf bank_mask:0xf // 000000002000: 6C0206FA FF015F02
+\ts_endpgm                                                   // 000000002008: BF810000
+"""
+
+
+def test_isa_check_detects_folded_row_broadcasts():
+    bad = isa_check.find_dpp_folds_in_listing(FOLD_SHAPE)
+    # the folded add and subrev; the moves and the quad_perm fold are allowed
+    assert [(n, i.split()[0]) for n, i in bad] == [("_ZN3hbx14g2d_add_group_iE", "v_add_u32_dpp"),
+                                                   ("_ZN3hbx8k_kernelE", "v_subrev_u32_dpp")]
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhbx.so not built")
+def test_library_has_no_folded_row_broadcast():
+    assert isa_check.find_dpp_folds(LIB) == []

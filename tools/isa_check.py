@@ -11,6 +11,9 @@ function's own loop: the wave never leaves the function (the printf trace of the
 entered the first exp-by-|x| and never returned).  Kernels are not affected (they end in
 s_endpgm; nothing lives in s[30:31]).
 
+``find_dpp_folds`` lists every VALU instruction other than a DPP move that carries row_newbcast
+(the folded row broadcast that gave wrong sums in round 5; see the comment above it).
+
 ``find_hazards`` lists every non-kernel function that performs a far branch through s[30:31]
 (an ``s_setpc_b64 s[30:31]`` that is preceded by an ``s_add_u32 s30`` of a relaxation sequence)
 and also returns through s[30:31].  tests/test_isa.py asserts the shipped library has none.
@@ -83,14 +86,46 @@ def find_hazards_in_listing(disasm: str):
     return bad
 
 
-def find_hazards(path: str):
+# A row broadcast folded into its consumer (VERDICT r5 item 2; DESIGN.md §4.2 "The DPP fold").  The
+# engine moves a lane's digit to its 16-lane row with `v_mov_b32_dpp ... row_newbcast:K`; LLVM's DPP
+# combiner may fold such a move into the VALU op that consumes it (`v_add_u32_dpp d, s, x
+# row_newbcast:K`), and in the group addition that folded form gave wrong sums on gfx950.  The moves
+# are pinned (groupd.hpp fqd_from_row), and this rule makes the build refuse any non-move VALU
+# instruction that carries row_newbcast, wherever the compiler might form one in a later build.
+_DPP_MOVES = ("v_mov_b32_dpp", "v_mov_b64_dpp")
+
+
+def find_dpp_folds_in_listing(disasm: str):
+    """[(function, instruction)] for every DPP-modified VALU op other than a move that uses
+    row_newbcast."""
+    bad = []
+    for name, body in _functions(disasm):
+        for ins in body:
+            op = ins.split(" ", 1)[0]
+            if op.endswith("_dpp") and op not in _DPP_MOVES and "row_newbcast" in ins:
+                bad.append((name, ins))
+    return bad
+
+
+def _listings(path: str):
     with tempfile.TemporaryDirectory() as tmp:
-        bad = []
         for co in _code_objects(path, tmp):
-            dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", co], capture_output=True,
+            yield subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", co], capture_output=True,
                                  text=True, check=True).stdout
-            bad += find_hazards_in_listing(dis)
-        return bad
+
+
+def find_hazards(path: str):
+    bad = []
+    for dis in _listings(path):
+        bad += find_hazards_in_listing(dis)
+    return bad
+
+
+def find_dpp_folds(path: str):
+    bad = []
+    for dis in _listings(path):
+        bad += find_dpp_folds_in_listing(dis)
+    return bad
 
 
 if __name__ == "__main__":
@@ -103,4 +138,11 @@ if __name__ == "__main__":
             rc = 1
         if not hz:
             print(f"{p}: no far branch through s[30:31] in any returning function")
+        folds = find_dpp_folds(p)
+        for name, ins in folds[:20]:
+            print(f"{p}: {name}: row broadcast folded into a VALU op: {ins}")
+        if folds:
+            rc = 1
+        else:
+            print(f"{p}: no row_newbcast outside v_mov_b32_dpp")
     sys.exit(rc)

@@ -25,7 +25,17 @@ def kernel_resources(path: str):
     """{kernel symbol: {field: int}} over every code object inside `path`."""
     res = {}
     with tempfile.TemporaryDirectory() as tmp:
-        for co in isa_check._code_objects(path, tmp):
+        with open(path, "rb") as fh:
+            head = fh.read(20)
+        # a device-only compile (--cuda-device-only) is the AMDGPU code object itself (e_machine 224)
+        direct = head[:4] == b"\x7fELF" and int.from_bytes(head[18:20], "little") == 224
+        if head.startswith(b"__CLANG_OFFLOAD_BUN"):  # a device-only compile without -fno-gpu-rdc bundling
+            co = os.path.join(tmp, "co")
+            subprocess.check_call([f"{isa_check.LLVM}/clang-offload-bundler", "--type=o",
+                                   f"--targets=hipv4-amdgcn-amd-amdhsa--{isa_check.ARCH}", f"--input={path}",
+                                   f"--output={co}", "--unbundle"])
+            path, direct = co, True
+        for co in ([path] if direct else isa_check._code_objects(path, tmp)):
             notes = subprocess.run([f"{isa_check.LLVM}/llvm-readelf", "--notes", co], capture_output=True,
                                    text=True).stdout
             for block in re.split(r"\n\s*- \.agpr_count", notes)[1:]:
