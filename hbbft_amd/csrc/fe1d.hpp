@@ -205,7 +205,7 @@ HBX_HD void fq6d_mul_acc_pm(fq6d& acc_p, fq6d& acc_m, const fq6d& a, Y y) {
 // X * Y, X in registers (reduced, or its conjugate), Y the packed value in slot y.  Reduced.
 // Karatsuba over w: c0 = X0 Y0 + v X1 Y1, c1 = (X0 + X1)(Y0 + Y1) - X0 Y0 - X1 Y1.
 #ifndef HBX_FE1_MUL_ORDER
-#define HBX_FE1_MUL_ORDER 1
+#define HBX_FE1_MUL_ORDER 0  // 1: the three-Fq6 order below (tools/build_variant.py measures it)
 #endif
 #if HBX_FE1_MUL_ORDER
 // The order keeps at most three Fq6 values beside a product's temporaries (the round-5 order held

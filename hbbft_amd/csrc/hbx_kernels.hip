@@ -444,6 +444,9 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
 // as k_verify_shares_ml (lane = sender i, blockIdx.y = proposer j).  Lanes whose status is not
 // SHARE_PENDING have nothing to do.  Step 6 turns SHARE_PENDING into HBX_SHARE_VALID / INVALID and,
 // in own-share mode, writes the own lane's verdict as Ciphertext::verify (k_verify_shares).
+#ifndef HBX_FE1_LANE_LDS
+#define HBX_FE1_LANE_LDS 0
+#endif
 template <int STEP>
 __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32_t n, uint8_t* __restrict__ valid,
                                             const uint8_t* __restrict__ ct_ok, uint32_t me,
@@ -459,7 +462,11 @@ __global__ void __launch_bounds__(64) k_fe1(uint32_t* __restrict__ gslot, uint32
       ct_valid[j] = !ct_ok[j] ? HBX_CT_UNDECODABLE : st == HBX_SHARE_VALID ? HBX_CT_VALID : HBX_CT_INVALID;
     return;
   }
+#if HBX_FE1_LANE_LDS
+  const lane_lds a{(lds_u32*)slots};  // the slot addressed afresh at every access (fe1d.hpp)
+#else
   lds_u32* a = (lds_u32*)(slots + threadIdx.x);
+#endif
   uint32_t* gf = gslot + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (3 * FE1_WORDS * 64) + threadIdx.x;
   uint32_t* gt = gf + FE1_WORDS * 64;
   uint32_t* gg = gt + FE1_WORDS * 64;

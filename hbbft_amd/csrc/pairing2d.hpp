@@ -584,7 +584,8 @@ constexpr int FE2_STEPS = (int)(sizeof(FE2_PROG) / sizeof(FE2_PROG[0]));
 // c0 = a0^2 - xi a1 a2, c1 = xi a2^2 - a0 a1, c2 = a1^2 - a0 a2, t = a0 c0 + xi (a2 c1 + a1 c2),
 // a^-1 = (c0, c1, c2) / t with t^-1 = conj(t) / (t0^2 + t1^2).  Input reduced; the reduced result
 // goes to `dst` (own half; it also parks (c0, c1, c2) meanwhile).
-__device__ __forceinline__ void fq6d_inv_to(const fq6d& a, lds_u32* dst, uint32_t stride) {
+template <class PD>
+__device__ __forceinline__ void fq6d_inv_to(const fq6d& a, PD dst, uint32_t stride) {
   fq2d t;
   {
     const fq2d c0 = fq2d_reduce(fq2d_sub(fq2d_sqr(a.c0), fq2d_mul_xi(fq2d_mul(a.c1, a.c2))));
@@ -617,9 +618,10 @@ __device__ __forceinline__ void fq6d_inv_to(const fq6d& a, lds_u32* dst, uint32_
 }
 
 // A = f^-1 = (f0 - f1 w) / (f0^2 - v f1^2) with f in B (own halves).
-__device__ __forceinline__ void op_inv(const slot2<lds_u32*>& A, const slot2<lds_u32*>& B, bool l1) {
+template <class PA>
+__device__ __forceinline__ void op_inv(const slot2<PA>& A, const slot2<lds_u32*>& B, bool l1) {
   const lds_u32* fb = B.half(l1 ? 1 : 0);
-  lds_u32* ao = A.half(l1 ? 1 : 0);
+  PA ao = A.half(l1 ? 1 : 0);
   fq6d S = fq6d_zero();  // lane 0: f0^2, lane 1: f1^2
   fq6d_mul_acc2(
       S, [&](int q) { return slot_get_fq2d(fb, B.stride, q); }, [&](int q) { return slot_get_fq2d(fb, B.stride, q); });
@@ -636,8 +638,8 @@ __device__ __forceinline__ void op_inv(const slot2<lds_u32*>& A, const slot2<lds
 // 16 squarings compressed; `degenerate` is then set (pair-uniformly) when a decompression met
 // g3 = 0, and the verdict is not valid -- the caller decides that pair again with KARA = false.
 __device__ __forceinline__ bool is_one2d(const fq6d& A, bool l1);
-template <bool KARA>
-__device__ __forceinline__ bool final_exp2d_is_one(const slot2<lds_u32*>& A, const slot2<lds_u32*>& B,
+template <bool KARA, class PA = lds_u32*>
+__device__ __forceinline__ bool final_exp2d_is_one(const slot2<PA>& A, const slot2<lds_u32*>& B,
                                                   const slot2<uint32_t*>& G1, const slot2<uint32_t*>& G2, bool l1,
                                                   bool& degenerate) {
   op_inv(A, B, l1);

@@ -4,8 +4,10 @@
   s[30:31] (tools/isa_check.py: the compiler defect behind the hung builds of rounds 2 and 3 --
   the function's return jumped back into its own loop).  The check is pinned on a listing
   shaped like the hung build's, so a silent parser change cannot make it pass vacuously.
-* No VALU instruction other than a DPP move carries a row broadcast (row_newbcast): the folded
-  form gave wrong sums on gfx950 (tools/isa_check.py find_dpp_folds, pinned on a listing with one).
+* No VALU instruction other than a DPP move carries a row broadcast (row_newbcast), and no
+  reversed-opcode VOP2 (v_subrev, v_lshlrev, ...) carries any DPP control: the reversed forms take
+  the lane selection on the wrong operand on gfx950 (tools/isa_check.py find_dpp_folds, pinned on a
+  listing with such folds; tools/microbench/dppfold.hip measures them).
 * Every DPP exchange helper carries its EXEC guard (hbbft_amd/csrc/dpp.hpp): the built code
   holds the trap instructions of those guards.
 """
@@ -76,6 +78,7 @@ FOLD_SHAPE = """
 \tv_add_u32_dpp v12, v33, v40 row_newbcast:3 row_mask:0xf bank_mask:0xf // 000000001008: 681850FA FF015321
 \tv_mov_b32_dpp v10, v33 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf // 000000001010: 7E1402FA FF000021
 \tv_sub_u32_dpp v13, v10, v41 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf // 000000001018: 6A1A52FA FF00B10A
+\tv_subrev_u32_dpp v14, v10, v42 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf // 000000001020: 6C1C54FA FF00550A
 \ts_setpc_b64 s[30:31]                                       // 000000001020: BE801D1E
 
 0000000000002000 <_ZN3hbx8k_kernelE>:
@@ -86,8 +89,10 @@ FOLD_SHAPE = """
 
 def test_isa_check_detects_folded_row_broadcasts():
     bad = isa_check.find_dpp_folds_in_listing(FOLD_SHAPE)
-    # the folded add and subrev; the moves and the quad_perm fold are allowed
+    # the folded row-broadcast add and subrev, and a reversed opcode under quad_perm; the moves and
+    # the quad_perm v_sub fold are allowed (measured exact, profiles/r06b_dppfold.txt)
     assert [(n, i.split()[0]) for n, i in bad] == [("_ZN3hbx14g2d_add_group_iE", "v_add_u32_dpp"),
+                                                   ("_ZN3hbx14g2d_add_group_iE", "v_subrev_u32_dpp"),
                                                    ("_ZN3hbx8k_kernelE", "v_subrev_u32_dpp")]
 
 

@@ -11,8 +11,8 @@ function's own loop: the wave never leaves the function (the printf trace of the
 entered the first exp-by-|x| and never returned).  Kernels are not affected (they end in
 s_endpgm; nothing lives in s[30:31]).
 
-``find_dpp_folds`` lists every VALU instruction other than a DPP move that carries row_newbcast
-(the folded row broadcast that gave wrong sums in round 5; see the comment above it).
+``find_dpp_folds`` lists every VALU instruction other than a DPP move that carries row_newbcast,
+and every reversed-opcode DPP instruction (measured wrong on gfx950; see the comment above it).
 
 ``find_hazards`` lists every non-kernel function that performs a far branch through s[30:31]
 (an ``s_setpc_b64 s[30:31]`` that is preceded by an ``s_add_u32 s30`` of a relaxation sequence)
@@ -86,23 +86,30 @@ def find_hazards_in_listing(disasm: str):
     return bad
 
 
-# A row broadcast folded into its consumer (VERDICT r5 item 2; DESIGN.md §4.2 "The DPP fold").  The
+# A lane move folded into its consumer (VERDICT r5 item 2; DESIGN.md §4.2 "The DPP fold").  The
 # engine moves a lane's digit to its 16-lane row with `v_mov_b32_dpp ... row_newbcast:K`; LLVM's DPP
-# combiner may fold such a move into the VALU op that consumes it (`v_add_u32_dpp d, s, x
-# row_newbcast:K`), and in the group addition that folded form gave wrong sums on gfx950.  The moves
-# are pinned (groupd.hpp fqd_from_row), and this rule makes the build refuse any non-move VALU
-# instruction that carries row_newbcast, wherever the compiler might form one in a later build.
+# combiner may fold such a move into the VALU op that consumes it, commuting a subtraction whose
+# broadcast operand is the subtrahend into the reversed opcode (`v_sub_u32 d, x, t` ->
+# `v_subrev_u32_dpp d, s, x`).  tools/microbench/dppfold.hip (profiles/r06b_dppfold.txt) measured on
+# gfx950: folded v_add / v_sub / v_xor are exact (bound_ctrl:1 included), but the REVERSED VOP2
+# opcodes (v_subrev_u32_dpp, v_lshlrev_b32_dpp) take the DPP lane selection on the other operand
+# (x of lane K minus s of the own lane), with row_newbcast and with quad_perm alike -- the wrong
+# sums of round 5.  The moves are pinned (groupd.hpp fqd_from_row), and the build refuses (a) any
+# reversed-opcode DPP instruction, whatever its control, and (b) any non-move VALU instruction that
+# carries row_newbcast (the broader rule VERDICT r5 asked for).
 _DPP_MOVES = ("v_mov_b32_dpp", "v_mov_b64_dpp")
 
 
 def find_dpp_folds_in_listing(disasm: str):
     """[(function, instruction)] for every DPP-modified VALU op other than a move that uses
-    row_newbcast."""
+    row_newbcast, and every reversed-opcode (…rev…) DPP op."""
     bad = []
     for name, body in _functions(disasm):
         for ins in body:
             op = ins.split(" ", 1)[0]
-            if op.endswith("_dpp") and op not in _DPP_MOVES and "row_newbcast" in ins:
+            if not op.endswith("_dpp") or op in _DPP_MOVES:
+                continue
+            if "row_newbcast" in ins or "rev_" in op:
                 bad.append((name, ins))
     return bad
 
@@ -144,5 +151,5 @@ if __name__ == "__main__":
         if folds:
             rc = 1
         else:
-            print(f"{p}: no row_newbcast outside v_mov_b32_dpp")
+            print(f"{p}: no row_newbcast outside v_mov_b32_dpp, no reversed-opcode DPP")
     sys.exit(rc)

@@ -10,6 +10,9 @@
 
 using namespace hbx;
 
+#ifndef PROBE_WAVES
+#define PROBE_WAVES 1  // min waves per SIMD the kernels are compiled for (2: at most 256 registers)
+#endif
 #ifndef PROBE_LANE_LDS
 #define PROBE_LANE_LDS 1  // 1: the slot addressed afresh (fe1d.hpp lane_lds), 0: a held pointer
 #endif
@@ -39,7 +42,7 @@ using namespace hbx;
 
 #if PROBE_ON(1)
 // one Fq12 product by the slot, `reps` times
-__global__ void __launch_bounds__(64) p_mul(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_mul(uint32_t* g, int reps) {
   PROBE_SLOTS;
   s1_copy<64, 64>(a, gg);
   HBX_SEQ();
@@ -55,7 +58,7 @@ __global__ void __launch_bounds__(64) p_mul(uint32_t* g, int reps) {
 
 #if PROBE_ON(2)
 // `reps` Granger-Scott squarings
-__global__ void __launch_bounds__(64) p_cyc(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_cyc(uint32_t* g, int reps) {
   PROBE_SLOTS;
   fq12d r = s1_get_fq12d<64>(gf);
 #pragma unroll 1
@@ -66,7 +69,7 @@ __global__ void __launch_bounds__(64) p_cyc(uint32_t* g, int reps) {
 
 #if PROBE_ON(3)
 // `reps` compressed squarings and the decompression
-__global__ void __launch_bounds__(64) p_kara(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_kara(uint32_t* g, int reps) {
   PROBE_SLOTS;
   fq12d r = s1_get_fq12d<64>(gf);
   fq12c c{r.c0.c1, r.c0.c2, r.c1.c0, r.c1.c2};
@@ -82,7 +85,7 @@ __global__ void __launch_bounds__(64) p_kara(uint32_t* g, int reps) {
 
 #if PROBE_ON(6)
 // `reps` compressed squarings alone
-__global__ void __launch_bounds__(64) p_kloop(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_kloop(uint32_t* g, int reps) {
   PROBE_SLOTS;
   fq12d r = s1_get_fq12d<64>(gf);
   fq12c c{r.c0.c1, r.c0.c2, r.c1.c0, r.c1.c2};
@@ -97,7 +100,7 @@ __global__ void __launch_bounds__(64) p_kloop(uint32_t* g, int reps) {
 
 #if PROBE_ON(7)
 // the decompression alone
-__global__ void __launch_bounds__(64) p_decomp(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_decomp(uint32_t* g, int reps) {
   PROBE_SLOTS;
   (void)reps;
   fq12c c{s1_get_fq2d<64>(gf, 0), s1_get_fq2d<64>(gf, 1), s1_get_fq2d<64>(gf, 2), s1_get_fq2d<64>(gf, 3)};
@@ -110,7 +113,7 @@ __global__ void __launch_bounds__(64) p_decomp(uint32_t* g, int reps) {
 
 #if PROBE_ON(8)
 // one Fq2 product alone (operands from the slots): the product's own register need
-__global__ void __launch_bounds__(64) p_fq2(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_fq2(uint32_t* g, int reps) {
   PROBE_SLOTS;
   (void)reps;
   const fq2d x = s1_get_fq2d<64>(gf, 0), y = s1_get_fq2d<64>(gf, 1);
@@ -120,7 +123,7 @@ __global__ void __launch_bounds__(64) p_fq2(uint32_t* g, int reps) {
 
 #if PROBE_ON(9)
 // one Fq6 product by a streamed operand into an accumulator
-__global__ void __launch_bounds__(64) p_fq6(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_fq6(uint32_t* g, int reps) {
   PROBE_SLOTS;
   (void)reps;
   const fq6d x = s1_get_half<64>(gf, 0);
@@ -132,9 +135,20 @@ __global__ void __launch_bounds__(64) p_fq6(uint32_t* g, int reps) {
 }
 #endif
 
+#if PROBE_ON(10)
+// `reps` dependent Fq inversions (field.hpp fq_inv_i: batched divsteps), the decompression's core
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_inv(uint32_t* g, int reps) {
+  PROBE_SLOTS;
+  fq x = fqd_to_fq(s1_get_fqd<64>(gf, 0));
+#pragma unroll 1
+  for (int k = 0; k < reps; k++) x = fq_add(fq_inv_i(x), fq_one());
+  s1_put_fqd<64>(gg, 0, fqd_from_fq(x));
+}
+#endif
+
 #if PROBE_ON(4)
 // one exp-by-|x| with the base in slot a
-__global__ void __launch_bounds__(64) p_exp(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_exp(uint32_t* g, int reps) {
   PROBE_SLOTS;
   (void)reps;
   s1_copy<64, 64>(a, gf);
@@ -149,7 +163,7 @@ __global__ void __launch_bounds__(64) p_exp(uint32_t* g, int reps) {
 
 #if PROBE_ON(5)
 // the F1 + F2 step kernel's body
-__global__ void __launch_bounds__(64) p_step12(uint32_t* g, int reps) {
+__global__ void __launch_bounds__(64, PROBE_WAVES) p_step12(uint32_t* g, int reps) {
   PROBE_SLOTS;
   (void)reps;
   bool deg = false;
@@ -164,7 +178,7 @@ __global__ void __launch_bounds__(64) p_step12(uint32_t* g, int reps) {
 // Timing harness (the pieces this build has, -DPROBE=k for one): each over 1,024 one-wave blocks (one wave per SIMD, the N=256 epoch's
 // share-check grid), HIP events, best of 3; per-unit microseconds = time / reps.
 int main() {
-  const int blocks = 1024;
+  const int blocks = 1024 * PROBE_WAVES;  // PROBE_WAVES waves per SIMD
   const size_t words = (size_t)blocks * 3 * FE1_WORDS * 64;
   std::vector<uint32_t> h(words);
   uint32_t s = 12345;
@@ -191,6 +205,9 @@ int main() {
 #if PROBE_ON(7)
       {"p_decomp (decompression)", p_decomp, 1},
 #endif
+#if PROBE_ON(10)
+      {"p_inv (Fq inversion)", p_inv, 8},
+#endif
 #if PROBE_ON(3)
       {"p_kara (48 sqr + decomp)", p_kara, 48},
 #endif
@@ -216,7 +233,9 @@ int main() {
       (void)hipEventElapsedTime(&ms, e0, e1);
       best = ms < best ? ms : best;
     }
-    printf("%-28s reps %3d  %8.3f ms  %8.2f us/unit\n", k.name, k.reps, best, best * 1e3 / k.reps);
+    // per unit of one wave-per-SIMD's work: time / (reps * waves per SIMD)
+    printf("%-28s reps %3d  waves/SIMD %d  %8.3f ms  %8.2f us/unit per 1024 waves\n", k.name, k.reps, PROBE_WAVES, best,
+           best * 1e3 / k.reps / PROBE_WAVES);
   }
   return 0;
 }
