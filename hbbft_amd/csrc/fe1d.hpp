@@ -365,13 +365,13 @@ HBX_HD fq12d karabina_decompress(const fq12c& c, bool& degenerate) {
     const fq2d den = fq2d_reduce(fq2d_dbl(fq2d_dbl(c.g3)));
     const fqd nrm = fqd_reduce(fqd_add(fqd_sqr(den.c0), fqd_sqr(den.c1)));
     HBX_SEQ();
-    const fq cn = fq_canon(fqd_to_fq(nrm));
-    degenerate = degenerate || fq_is_zero(cn);
+    bool zero;
 #if HBX_KARA_INV_CALL
-    const fqd ni = fqd_from_fq(fq_inv(cn));  // out of line (field.hpp): its loop sees only its own state
+    const fqd ni = fqd_inv_ni(nrm, zero);  // out of line (fieldd.hpp): its loop sees only its own state
 #else
-    const fqd ni = fqd_from_fq(fq_inv_i(cn));
+    const fqd ni = fqd_inv(nrm, zero);
 #endif
+    degenerate = degenerate || zero;
     HBX_SEQ();
     g4 = fq2d_mul(num, fq2d_mul_fq(fq2d_conj(den), ni));
   }
@@ -482,7 +482,8 @@ HBX_HD void fq6d_inv_to_slot(const fq6d& a, P y) {
   HBX_SEQ();
   const fqd nrm = fqd_reduce(fqd_add(fqd_sqr(t.c0), fqd_sqr(t.c1)));
   HBX_SEQ();
-  const fqd ni = fqd_from_fq(fq_inv_i(fqd_to_fq(nrm)));
+  bool zero;  // (N(f) != 0: f is a nonzero Miller value)
+  const fqd ni = fqd_inv(nrm, zero);
   HBX_SEQ();
   const fq2d ti = fq2d_mul_fq(fq2d_conj(t), ni);
 #pragma unroll 1

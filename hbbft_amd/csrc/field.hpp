@@ -474,10 +474,13 @@ HBX_HDNI fq fq_pow_const(const fq& a, const uint32_t* e) {
 // Fixed step count and selects only: every lane of a wave runs the same instructions (~30k VALU
 // ops for N = 12, against ~150k for the bit-by-bit binary Euclid this replaced, whose
 // data-dependent branch split the wave).  x = 0 gives 0.
-HBX_HD void divsteps30(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32_t& v, int32_t& q, int32_t& r) {
+// NS steps (NS <= 30; the digit-form inversion of fieldd.hpp runs 28 on a 28-bit digit)
+template <int NS>
+HBX_HD void divsteps_n(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32_t& v, int32_t& q, int32_t& r) {
   int32_t uu = 1, vv = 0, qq = 0, rr = 1;
-#pragma unroll 6
-  for (int i = 0; i < 30; i++) {
+  constexpr int UR = NS % 7 == 0 ? 7 : 6;  // 30 steps: 5 x 6 as before; 28: 4 x 7
+#pragma unroll UR
+  for (int i = 0; i < NS; i++) {
     const bool godd = (g & 1u) != 0;
     const bool sw = godd && delta > 0;
     const uint32_t nf = sw ? g : f;
@@ -497,6 +500,9 @@ HBX_HD void divsteps30(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32
   v = vv;
   q = qq;
   r = rr;
+}
+HBX_HD void divsteps30(int32_t& delta, uint32_t f, uint32_t g, int32_t& u, int32_t& v, int32_t& q, int32_t& r) {
+  divsteps_n<30>(delta, f, g, u, v, q, r);
 }
 // out = (ca a + cb b) / 2^30 for L-limb two's complement a, b (top limb signed); exact.
 template <int L>

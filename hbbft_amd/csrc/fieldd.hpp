@@ -650,6 +650,101 @@ HBX_HD fq fqd_to_fq(const fqd& a) {
 }
 HBX_HD fq2d fq2d_from_fq2(const fq2& a) { return fq2d{fqd_from_fq(a.c0), fqd_from_fq(a.c1)}; }
 
+// ---- Fq inversion on the digits themselves ---------------------------------------------------------
+// field.hpp binv_limbs' half-delta divsteps (Bernstein-Yang; the step bound of libsecp256k1's
+// safegcd analysis), batched 28 at a time so that a batch's division by 2^28 is a shift of the
+// digit index: 28 divsteps on digit 0 of f and g give the matrix T (|entries| <= 2^28), then
+// (f, g) <- T (f, g) / 2^28 exactly and (d, e) <- (T (d, e) + k p) / 2^28 with k = -(T (d, e))_0
+// p^-1 mod 2^28, one signed v_mad_i64_i32 per digit product and one carry step per digit.  The
+// 12-limb route (fqd_to_fq, fq_canon, binv_limbs on 32-bit limbs, whose signed x unsigned limb
+// products the compiler expands, fq_mul by R^3, fqd_from_fq) measured 100.5 us per lone wave
+// (profiles/r06i_fq_inversion.txt).  d, e grow by at most p per batch (|d'| <= max(|d|, |e|) + p:
+// 33 batches stay below 34 p, digit 13 below 2^22), f, g stay within [-p, p].
+// In: a in digit Montgomery form (x R', any normalised-range value); out: x^-1 R' (normalised,
+// value in (-p, 2p)), 0 for x = 0 (zero set).
+HBX_HD fqd fqd_addp_if(const fqd& v, bool add, int sign) {  // v + sign p when add, carry-normalised
+  fqd r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const int32_t t = v.d[i] + (add ? sign * (int32_t)FQ_P28[i] : 0) + c;
+    if (i < 13) {
+      r.d[i] = t & DMASK;
+      c = t >> 28;
+      HBX_LAUNDER(r.d[i]);
+    } else {
+      r.d[i] = t;
+    }
+  }
+  return r;
+}
+// the representative of v in [0, p), digits normalised (v's value within (-2p, 3p))
+HBX_HD fqd fqd_canon(const fqd& v_) {
+  fqd v = fqd_norm(v_);
+  v = fqd_addp_if(v, v.d[13] < 0, 1);
+  v = fqd_addp_if(v, v.d[13] < 0, 1);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const fqd t = fqd_addp_if(v, true, -1);
+    const bool ge = t.d[13] >= 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) v.d[i] = ge ? t.d[i] : v.d[i];
+  }
+  return v;
+}
+// (ca a + cb b [+ k p]) / 2^28, exact; a, b digits normalised; |ca| + |cb| <= 2^28
+template <bool MODP>
+HBX_HD fqd fqd_lincomb28(const fqd& a, const fqd& b, int32_t ca, int32_t cb) {
+  int64_t acc = (int64_t)ca * a.d[0] + (int64_t)cb * b.d[0];
+  int32_t k = 0;
+  if (MODP) {
+    k = (int32_t)(((uint32_t)acc * FQ_INV28) & (uint32_t)DMASK);
+    acc += (int64_t)k * (int64_t)FQ_P28[0];  // low 28 bits now zero
+  }
+  acc >>= 28;
+  fqd r;
+#pragma unroll
+  for (int i = 1; i < 14; i++) {
+    acc += (int64_t)ca * a.d[i];
+    acc += (int64_t)cb * b.d[i];
+    if (MODP) acc += (int64_t)k * (int64_t)FQ_P28[i];
+    r.d[i - 1] = (int32_t)((uint32_t)acc & (uint32_t)DMASK);
+    HBX_LAUNDER(r.d[i - 1]);
+    acc >>= 28;
+  }
+  r.d[13] = (int32_t)acc;
+  return r;
+}
+HBX_HD fqd fqd_inv(const fqd& a, bool& zero) {
+  constexpr int BATCHES = ((45907 * 381 + 26313) / 19929 + 28 + 27) / 28;  // hddivsteps bound + one batch
+  fqd g = fqd_canon(a), f, d = fqd_zero(), e = fqd_zero();
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    f.d[i] = (int32_t)FQ_P28[i];
+    nz |= (uint32_t)g.d[i];
+  }
+  zero = nz == 0;
+  e.d[0] = 1;
+  int32_t delta = 1;  // 2 delta, delta = 1/2
+#pragma unroll 1
+  for (int b = 0; b < BATCHES; b++) {
+    int32_t u, v, q, r;
+    divsteps_n<28>(delta, (uint32_t)f.d[0], (uint32_t)g.d[0], u, v, q, r);
+    const fqd nf = fqd_lincomb28<false>(f, g, u, v);
+    const fqd ng = fqd_lincomb28<false>(f, g, q, r);
+    const fqd nd = fqd_lincomb28<true>(d, e, u, v);
+    e = fqd_lincomb28<true>(d, e, q, r);
+    f = nf;
+    g = ng;
+    d = nd;
+  }
+  // g = 0, f = +-1 (f = p, d = 0 for x = 0): x^-1 = f d, then times R'^3 / R'
+  const bool fneg = f.d[0] != 1;
+  return fqd_mul(fneg ? fqd_neg(d) : d, fqd_const(FQD_R3));
+}
+HBX_HDNI fqd fqd_inv_ni(const fqd& a, bool& zero) { return fqd_inv(a, zero); }
+
 // a^e (e a 384-bit constant, 12 LE words) in the digit tower: field.hpp fq_pow_const's 4-bit
 // fixed windows, with the squarings and products as fqd_sqr / fqd_mul (no re-cutting of 12 limbs
 // into digits around every product).  In and out in field.hpp's 12-limb form.  The hash chains'

@@ -362,8 +362,28 @@ HBX_HD fq12d miller_loop2_scaled_d(const line_pre_d* LA, bool useA, const line_p
 }
 // (x / y, 1 / y) of the two affine G1 points into the slot (words 0..3), one Fq inversion for both
 // (Montgomery's trick); a point at infinity contributes 1 (its pair is not used)
+#ifndef HBX_ML_INV
+#define HBX_ML_INV 0  // the scalars' inversion: 0 12-limb (inline), 1 digit form inline, 2 digit form out of line
+#endif
 HBX_HD void park_scaled_points(lds_u32* park, const fq& ax, const fq& ay, bool ainf, const fq& bx, const fq& by,
                                bool binf) {
+#if HBX_ML_INV
+  // in the digit form throughout (fieldd.hpp fqd_inv; HBX_ML_INV 2: out of line)
+  const fqd ya = ainf ? fqd_const(FQD_ONE) : fqd_from_fq(ay), yb = binf ? fqd_const(FQD_ONE) : fqd_from_fq(by);
+  bool zero;
+#if HBX_ML_INV == 2
+  const fqd inv = fqd_inv_ni(fqd_mul(ya, yb), zero);
+#else
+  const fqd inv = fqd_inv(fqd_mul(ya, yb), zero);
+#endif
+  const fqd ua = fqd_mul(inv, yb), ub = fqd_mul(inv, ya);
+  park_put_fqd(park, 0, fqd_mul(fqd_from_fq(ax), ua));
+  park_put_fqd(park, 1, ua);
+  park_put_fqd(park, 2, fqd_mul(fqd_from_fq(bx), ub));
+  park_put_fqd(park, 3, ub);
+#else
+  // the 12-limb inversion: inlined into the Miller kernel, the digit form's raised its time 8.31 ->
+  // 8.48 ms (profiles/r06k_kernel_stats.txt); see HBX_ML_INV
   const fq ya = ainf ? fq_one() : ay, yb = binf ? fq_one() : by;
   const fq inv = fq_inv_i(fq_mul(ya, yb));
   const fq ua = fq_mul(inv, yb), ub = fq_mul(inv, ya);
@@ -371,6 +391,7 @@ HBX_HD void park_scaled_points(lds_u32* park, const fq& ax, const fq& ay, bool a
   park_put_fqd(park, 1, fqd_from_fq(ua));
   park_put_fqd(park, 2, fqd_from_fq(fq_mul(bx, ub)));
   park_put_fqd(park, 3, fqd_from_fq(ub));
+#endif
 }
 
 // miller_loop_gen_d with (qx, qy, bx, by) parked in this lane's LDS slot (free until the final

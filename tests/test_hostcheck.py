@@ -340,6 +340,46 @@ def test_hddivsteps_bound():
         assert worst <= bound, (mod, worst, bound)
 
 
+def _digits14(v):
+    """v (any integer) as 14 normalised signed digits: digits 0..12 in [0, 2^28), digit 13 the rest."""
+    ds = []
+    for _ in range(13):
+        ds.append(v & 0xFFFFFFF)
+        v >>= 28
+    return ds + [v]
+
+
+def test_fqd_inv_digit_form(hc):
+    """fieldd.hpp fqd_inv (divsteps on the 28-bit digits, the final exponentiation's and the Miller
+    kernels' inversions since round 6) against Python's modular inverse: the input is x R' (R' =
+    2^392) as any representative in (-2p, 3p), the output must be x^-1 R' mod p, normalised digits,
+    value in (-p, 2p); x = 0 gives 0 with the zero flag."""
+    rnd = random.Random(28)
+    p, rr = bls.P, 1 << 392
+    xs = [0, 1, 2, 3, p - 1, p - 2, (p + 1) // 2] + [rnd.randrange(p) for _ in range(400)] + _slow_gcd_inputs(p)[:200]
+    for n, x in enumerate(xs):
+        a = x * rr % p + p * rnd.choice((-2, -1, 0, 1, 2))  # any representative in (-2p, 3p)
+        if a <= -2 * p or a >= 3 * p:
+            a = x * rr % p
+        ad = (ctypes.c_int32 * 14)(*[d if d < (1 << 31) else d - (1 << 32) for d in _digits14(a)])
+        out = (ctypes.c_int32 * 14)()
+        z = hc.hc_fqd_inv(ad, out)
+        got = sum(int(out[i]) << (28 * i) for i in range(14))
+        assert all(0 <= out[i] < (1 << 28) for i in range(13)), x
+        assert -p < got < 2 * p, x
+        if x == 0:
+            assert z == 1 and got % p == 0
+        else:
+            assert z == 0 and got % p == pow(x, -1, p) * rr % p, (n, x)
+    # the divsteps' slowest inputs as the canonical value the steps run on: out = a^-1 R'^2
+    for a in _slow_gcd_inputs(p):
+        ad = (ctypes.c_int32 * 14)(*[d if d < (1 << 31) else d - (1 << 32) for d in _digits14(a % p)])
+        out = (ctypes.c_int32 * 14)()
+        hc.hc_fqd_inv(ad, out)
+        got = sum(int(out[i]) << (28 * i) for i in range(14))
+        assert got % p == pow(a, -1, p) * rr * rr % p, a
+
+
 def test_binv_divsteps(hc):
     """binv_limbs (batched Bernstein-Yang divsteps, every inversion of the kernels) against
     Python's modular inverse, mod p and mod r, on random and edge values (0 -> 0)."""

@@ -316,6 +316,16 @@ int hc_lines_jac_cmp(const uint8_t* in96, const uint8_t* z0_48, const uint8_t* z
   }
   return bad;
 }
+// fieldd.hpp fqd_inv on 14 signed digits (any value in (-2p, 3p)): out = the 14 result digits,
+// returns the zero flag
+int hc_fqd_inv(const int32_t* a14, int32_t* out14) {
+  fqd a;
+  for (int i = 0; i < 14; i++) a.d[i] = a14[i];
+  bool zero = false;
+  const fqd r = fqd_inv(a, zero);
+  for (int i = 0; i < 14; i++) out14[i] = r.d[i];
+  return zero ? 1 : 0;
+}
 // binv_limbs (batched divsteps) on canonical little-endian limbs: which = 0 mod p (12 limbs),
 // 1 mod r (8 limbs)
 int hc_binv(const uint32_t* x, int which, uint32_t* out) {

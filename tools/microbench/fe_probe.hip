@@ -139,10 +139,19 @@ __global__ void __launch_bounds__(64, PROBE_WAVES) p_fq6(uint32_t* g, int reps) 
 // `reps` dependent Fq inversions (field.hpp fq_inv_i: batched divsteps), the decompression's core
 __global__ void __launch_bounds__(64, PROBE_WAVES) p_inv(uint32_t* g, int reps) {
   PROBE_SLOTS;
-  fq x = fqd_to_fq(s1_get_fqd<64>(gf, 0));
+#if PROBE_INV_DIGITS
+  fqd x = s1_get_fqd<64>(gf, 0);  // fieldd.hpp fqd_inv (divsteps on the 28-bit digits)
+  bool z = false;
+#pragma unroll 1
+  for (int k = 0; k < reps; k++) x = fqd_norm(fqd_add(fqd_inv(x, z), fqd_const(FQD_ONE)));
+  s1_put_fqd<64>(gg, 0, x);
+  if (z) gg[64] = 1;
+#else
+  fq x = fqd_to_fq(s1_get_fqd<64>(gf, 0));  // field.hpp fq_inv_i (12-limb divsteps)
 #pragma unroll 1
   for (int k = 0; k < reps; k++) x = fq_add(fq_inv_i(x), fq_one());
   s1_put_fqd<64>(gg, 0, fqd_from_fq(x));
+#endif
 }
 #endif
 
