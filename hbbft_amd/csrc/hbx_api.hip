@@ -1381,8 +1381,9 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
   const int lanes = c->verify_lanes == 1 || c->verify_lanes == 2 ? c->verify_lanes
                     : waves1 < (size_t)VERIFY_FILL_WAVES ? 2 : 1;
   c->coin_lanes_used = lanes;
-  if (lanes == 1 && !c->coin_lines_ready) {
-    // H''s prepared lines for the one-lane kernel (wave-uniform loads)
+  if (!c->coin_lines_ready) {
+    // H''s prepared lines (wave-uniform loads): the one-lane kernel's mixed loop, and since round 6
+    // the two-lane kernel's H' pair (its lanes then generate only sigma's lines, together)
     timed t_(c, HBX_K_PREPARE_LINES, s);
     hipLaunchKernelGGL(k_prepare_lines<true>, dim3((count * LINE_K + 63) / 64), dim3(64), 0, s, c->coin_Hp.as<g2a>(), count,
                        c->coin_lines_d.as<line_pre_d>(), c->coin_scratch.as<fq2d>(), nullptr, 0u, nullptr, nullptr, nullptr, 1u,
@@ -1414,7 +1415,7 @@ static int verify_sig_impl(hbx_ctx* c, const uint8_t* d_sig96, const uint8_t* d_
       for (uint32_t retry = 0; retry < 2; retry++) {
         hipLaunchKernelGGL(k_verify_sig_shares2, grid, dim3(64), 0, s, c->coin_Hp.as<g2a>(), c->pk.as<g1a>(), c->n_keys,
                            c->coin_sig.as<g2a>(), c->coin_sig_st.as<int32_t>(), d_present, n, c->coin_valid.as<uint8_t>(),
-                           c->gslot.as<uint32_t>(), retry);
+                           c->gslot.as<uint32_t>(), retry, c->coin_lines_d.as<line_pre_d>());
         HIPCHK(c, hipGetLastError());
         if (retry == 0)
           hipLaunchKernelGGL(k_verify_sig_shares2_fe<true>, grid, dim3(64), 0, s, n, c->coin_valid.as<uint8_t>(),

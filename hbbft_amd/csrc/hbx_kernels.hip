@@ -568,12 +568,16 @@ __global__ void __launch_bounds__(64) k_verify_shares2(const g1a* __restrict__ S
 // Miller loops (sigma's membership in G2 from lane 1's T) and the pair product, and leaves the
 // product's halves in the pair's global slot G1 with status SHARE_PENDING; k_verify_sig_shares2_fe
 // runs the two-lane final exponentiation of the pending pairs.  Same grid for both.
+// Since round 6 H''s lines come prepared (Hlines: [instance][68], k_prepare_lines +
+// k_normalise_lines once per instance) and the pair generates sigma's lines together
+// (pairing2d.hpp miller_gen2s); the round-5 schedule -- each lane generating its own pair's lines
+// (miller_gen2d) -- remains for Hlines = nullptr.
 __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict__ H, const g1a* __restrict__ pk,
                                                            uint32_t n_keys, const g2a* __restrict__ sig,
                                                            const int32_t* __restrict__ sig_status,
                                                            const uint8_t* __restrict__ present, uint32_t n,
                                                            uint8_t* __restrict__ valid, uint32_t* __restrict__ gslot,
-                                                           uint32_t retry) {
+                                                           uint32_t retry, const line_pre_d* __restrict__ Hlines) {
   __shared__ uint32_t region[LDS2_DWORDS * 64];
   const int lane = (int)(threadIdx.x & 63);
   const bool l1 = (lane & 1) != 0;
@@ -601,7 +605,19 @@ __global__ void __launch_bounds__(64) k_verify_sig_shares2(const g2a* __restrict
     lds_u32* reg = (lds_u32*)region;
     const int pl = lane & ~1;
     g2jd T;
-    const fq6d f = miller_gen2d(qp, fqd_from_fq(P.x), fqd_from_fq(P.y), use, l1, (lds2)(reg + lane), reg + pl, T);
+    fq6d f;
+    if (Hlines) {
+      // both lanes: pk_i's scalars (lane 0 1 / y, lane 1 x / y), sigma at -[m] g1 (pair-uniform flags)
+      const g1a pki = pk[i];
+      const g2a Hq = H[inst], Sq = sig[idx];
+      fqd sc = fqd_zero();
+      if (!pki.inf) sc = point_scalar2d(pki, false, l1);
+      f = miller_gen2s(Hlines + (size_t)inst * MILLER_LINES, sc, !(Hq.inf || pki.inf), sig + idx,
+                       fqd_from_fq(fq_from_const(G1_MGEN_X)), fqd_from_fq(fq_neg(fq_from_const(G1_MGEN_Y))), !Sq.inf,
+                       l1, (lds2)(reg + lane), reg + pl, T);
+    } else {
+      f = miller_gen2d(qp, fqd_from_fq(P.x), fqd_from_fq(P.y), use, l1, (lds2)(reg + lane), reg + pl, T);
+    }
     // sigma's membership in G2 from lane 1's T = [|x|] sigma (decode skipped it); lane 0's is H's
     tf = !l1 || g2_torsion_free_from_T(T, Q);
     // this lane's half of f_A f_B to the pair's global slot

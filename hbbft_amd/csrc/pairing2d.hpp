@@ -701,9 +701,15 @@ constexpr int MG_PARK = 78;
 // lane 0 A0 L0 + v^2 c4 A1, lane 1 A1 L0 + v c4 A0 (L0 = c0 + c1 v; w^2 = v).  8 Fq2 products per
 // lane against the one-lane sparse product's 13; the partner's half comes over one coefficient at
 // a time.  Reduced output.
+// C4ONE: the line is c0 + c1 v + v w (a prepared line scaled by 1 / y_P, the coin's H' lines since
+// round 6): E = A_(1-k) itself, no c4 products.
+template <bool C4ONE = false>
 __device__ __forceinline__ fq6d line2d_f2(const fq6d& A, bool l1, const lds_u32* ln) {
   fq6d acc;  // v^(2-k) c4 A_(1-k), then + A_k L0 (fieldd.hpp fq6d_mul_by_01's Karatsuba)
-  {
+  if (C4ONE) {
+    const fq6d vE = fq6d_mul_v(fq6d{xchg_t(A.c0), xchg_t(A.c1), xchg_t(A.c2)});
+    acc = sel_t(l1, vE, fq6d_mul_v(vE));
+  } else {
     const fq2d c4 = slot_get_fq2d(ln, 64u, 2);
     fq6d E;
     E.c0 = fq2d_mul(xchg_t(A.c0), c4);
@@ -788,6 +794,144 @@ __device__ __forceinline__ fq6d miller_gen2d(const g2a* q, const fqd& px, const 
   // |x| = 0xd201000000010000: the doubling steps i = 62..0 in runs, an addition step after each run
   // but the last (bits 62, 60, 57, 48, 16).  The addition is an out-of-line call, kept out of the
   // runs' loops: inside the loop the values live across it spilled (139 VGPRs).
+  static_assert(BLS_X == 0xd201000000010000ull, "the runs below follow |x|'s bits");
+  constexpr int RUN[6] = {1, 2, 3, 9, 32, 16};
+  bool first = true;
+#pragma unroll 1
+  for (int r = 0; r < 6; r++) {
+#pragma unroll 1
+    for (int t = 0; t < RUN[r]; t++) {
+      if (!first) f = sqr2d<true>(f, l1, lds);
+      first = false;
+      step(false);
+    }
+    if (r < 5) step(true);
+  }
+  HBX_SEQ();
+  {
+    const fq6d t = slot_get_fq6d(park, 64u);
+    Tout = g2jd{t.c0, t.c1, t.c2};
+  }
+  return conj2d(f, l1);
+}
+
+// ---- the coin check with H''s lines prepared once per instance (round 6) ---------------------
+// The 128 checks of an instance share H': its 68 Miller lines are prepared once (k_prepare_lines +
+// k_normalise_lines, as the decryption checks' are) and each pair only loads them, scaled by
+// 1 / y_pk (c4 = 1: line2d_f2<true> skips the three c4 products).  Both lanes then generate
+// sigma's lines TOGETHER: each doubling step is split into rounds of one Fq2 product per lane
+// whose results the pair exchanges (6 rounds instead of pairingd.hpp line_dbl_step_di's 11
+// products), so both lanes hold sigma's T and line.
+
+// one product round on the pair: lane 0 computes a0 b0, lane 1 a1 b1; both get (r0, r1)
+__device__ __forceinline__ void round2_mul(bool l1, const fq2d& a0, const fq2d& b0, const fq2d& a1, const fq2d& b1,
+                                           fq2d& r0, fq2d& r1) {
+  const fq2d mine = fq2d_mul(sel_t(l1, a1, a0), sel_t(l1, b1, b0));
+  const fq2d other = xchg_t(mine);
+  r0 = sel_t(l1, other, mine);
+  r1 = sel_t(l1, mine, other);
+}
+__device__ __forceinline__ void round2_sqr(bool l1, const fq2d& a0, const fq2d& a1, fq2d& r0, fq2d& r1) {
+  const fq2d mine = fq2d_sqr(sel_t(l1, a1, a0));
+  const fq2d other = xchg_t(mine);
+  r0 = sel_t(l1, other, mine);
+  r1 = sel_t(l1, mine, other);
+}
+__device__ __forceinline__ void round2_mul_fq(bool l1, const fq2d& a0, const fqd& s0, const fq2d& a1, const fqd& s1,
+                                              fq2d& r0, fq2d& r1) {
+  const fq2d mine = fq2d_mul_fq(sel_t(l1, a1, a0), sel_t(l1, s1, s0));
+  const fq2d other = xchg_t(mine);
+  r0 = sel_t(l1, other, mine);
+  r1 = sel_t(l1, mine, other);
+}
+// pairingd.hpp line_dbl_step_di on the pair (both lanes hold T; the same T', c0, c1, c2 result):
+// A = X^2 | B = Y^2;  ZZ = Z^2 | YZ;  C = B^2 | F = E^2;  (X + B)^2 | E X;  E ZZ | Z3 ZZ;  E (D - X3)
+__device__ __forceinline__ void line_dbl_step_2s(g2jd& T, bool l1, fq2d& c0, fq2d& c1, fq2d& c2) {
+  fq2d A, B, ZZ, YZ, C, F, S, EX, EZZ;
+  round2_sqr(l1, T.x, T.y, A, B);
+  HBX_SEQ();
+  round2_mul(l1, T.z, T.z, T.y, T.z, ZZ, YZ);
+  HBX_SEQ();
+  const fq2d E = fq2d_norm(fq2d_add(fq2d_dbl(A), A));
+  const fq2d XB = fq2d_add(T.x, B);
+  const fq2d Z3 = fq2d_reduce(fq2d_dbl(YZ));
+  round2_sqr(l1, B, E, C, F);
+  HBX_SEQ();
+  round2_mul(l1, XB, XB, E, T.x, S, EX);
+  HBX_SEQ();
+  round2_mul(l1, E, ZZ, Z3, ZZ, EZZ, c2);
+  HBX_SEQ();
+  c0 = fq2d_reduce(fq2d_sub(EX, fq2d_dbl(B)));
+  c1 = fq2d_neg(EZZ);
+  const fq2d D = fq2d_reduce(fq2d_dbl(fq2d_sub(fq2d_sub(S, A), C)));
+  const fq2d X3 = fq2d_reduce(fq2d_sub(F, fq2d_dbl(D)));
+  const fq2d C8 = fq2d_dbl(fq2d_reduce(fq2d_dbl(fq2d_dbl(C))));
+  const fq2d Y3 = fq2d_reduce(fq2d_sub(fq2d_mul(E, fq2d_sub(D, X3)), C8));
+  T = g2jd{X3, Y3, Z3};
+}
+
+// The coin check's two Miller loops on a pair with H''s prepared lines LH (68, Miller order; the
+// instance's, wave-uniform): lane 0 holds s = 1 / y_pk, lane 1 s = x_pk / y_pk (point_scalar2d of
+// pk_i); useH false: the H' pair contributes 1.  sigma (*q) at -[m] g1 = (px, py) in digit form;
+// useS false: sigma's lines are 1.  Returns this lane's half of f_H f_sigma (conjugated for x < 0);
+// T = [|x|] sigma on both lanes.  LDS: lane 0's column holds H''s scaled line (words 0..55), lane
+// 1's sigma's (c0, c1 px, c2 py); both columns' park (words MG_PARK..) holds whichever of T and f is
+// idle, as in miller_gen2d.
+__device__ __forceinline__ fq6d miller_gen2s(const line_pre_d* LH, const fqd& s, bool useH, const g2a* q,
+                                             const fqd& px, const fqd& py, bool useS, bool l1, lds2 lds,
+                                             const lds_u32* pair0, g2jd& Tout) {
+  const fq2d one{fqd_const(FQD_ONE), fqd_zero()}, zero{fqd_zero(), fqd_zero()};
+  lds_u32* park = lds + MG_PARK * 64;
+  {
+    const g2a Q = *q;
+    slot_put_fq6d(park, 64u, fq6d{fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), one});  // T
+  }
+  fq6d f = sel_t(l1, fq6d_zero(), fq6d_one());
+  int k = 0;
+  auto step = [&](bool add) __attribute__((always_inline)) {
+    HBX_SEQ();
+    g2jd T;
+    {
+      const fq6d t = slot_get_fq6d(park, 64u);
+      T = g2jd{t.c0, t.c1, t.c2};
+    }
+    HBX_SEQ();
+    slot_put_fq6d(park, 64u, f);
+    HBX_SEQ();
+    fq2d c0, c1, c2;
+    if (!add) {
+      line_dbl_step_2s(T, l1, c0, c1, c2);
+    } else {
+      const g2a Q = *q;  // both lanes run sigma's addition step (the same values)
+      line_add_step_call(T, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), c0, c1, c2);
+    }
+    HBX_SEQ();
+    // sigma's (c1 px | c2 py) and H''s scaled (h0 / y | h1 x / y), one product per lane each
+    fq2d c1p, c2p, h0s, h1s;
+    round2_mul_fq(l1, c1, px, c2, py, c1p, c2p);
+    HBX_SEQ();
+    {
+      const line_pre_d L = ld_uniform(LH + k);
+      round2_mul_fq(l1, L.c0, s, L.c1, s, h0s, h1s);
+    }
+    k++;
+    HBX_SEQ();
+    // lane 0's column: H''s line; lane 1's: sigma's (each lane writes its own column)
+    slot_put_fq2d(lds, 64u, 0, sel_t(l1, sel_t(useS, c0, one), h0s));
+    slot_put_fq2d(lds, 64u, 1, sel_t(l1, sel_t(useS, c1p, zero), h1s));
+    slot_put_fq2d(lds, 64u, 2, sel_t(useS, c2p, zero));  // (lane 0's word 2 unused: c4 = 1)
+    HBX_SEQ();
+    f = slot_get_fq6d(park, 64u);
+    HBX_SEQ();
+    slot_put_fq6d(park, 64u, fq6d{T.x, T.y, T.z});
+    HBX_SEQ();
+    {
+      const fq6d fh = line2d_f2<true>(f, l1, pair0);
+      f = sel_t(useH, fh, f);  // pair-uniform (both lanes know pk_i and H')
+    }
+    HBX_SEQ();
+    f = line2d_f2(f, l1, pair0 + 1);
+  };
   static_assert(BLS_X == 0xd201000000010000ull, "the runs below follow |x|'s bits");
   constexpr int RUN[6] = {1, 2, 3, 9, 32, 16};
   bool first = true;

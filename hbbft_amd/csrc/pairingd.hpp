@@ -363,7 +363,7 @@ HBX_HD fq12d miller_loop2_scaled_d(const line_pre_d* LA, bool useA, const line_p
 // (x / y, 1 / y) of the two affine G1 points into the slot (words 0..3), one Fq inversion for both
 // (Montgomery's trick); a point at infinity contributes 1 (its pair is not used)
 #ifndef HBX_ML_INV
-#define HBX_ML_INV 0  // the scalars' inversion: 0 12-limb (inline), 1 digit form inline, 2 digit form out of line
+#define HBX_ML_INV 2  // the scalars' inversion: 0 12-limb (inline), 1 digit form inline, 2 digit form out of line
 #endif
 HBX_HD void park_scaled_points(lds_u32* park, const fq& ax, const fq& ay, bool ainf, const fq& bx, const fq& by,
                                bool binf) {
@@ -382,8 +382,9 @@ HBX_HD void park_scaled_points(lds_u32* park, const fq& ax, const fq& ay, bool a
   park_put_fqd(park, 2, fqd_mul(fqd_from_fq(bx), ub));
   park_put_fqd(park, 3, ub);
 #else
-  // the 12-limb inversion: inlined into the Miller kernel, the digit form's raised its time 8.31 ->
-  // 8.48 ms (profiles/r06k_kernel_stats.txt); see HBX_ML_INV
+  // the 12-limb inversion (round 5).  The digit form inlined raised the Miller kernel 8.31 -> 8.48 ms
+  // (profiles/r06k_kernel_stats.txt); out of line (HBX_ML_INV 2, the default) it is neutral to
+  // slightly faster (verify 16.96 -> 16.94 ms, coin 13.37 -> 13.33 ms, profiles/r06l_variants.txt)
   const fq ya = ainf ? fq_one() : ay, yb = binf ? fq_one() : by;
   const fq inv = fq_inv_i(fq_mul(ya, yb));
   const fq ua = fq_mul(inv, yb), ub = fq_mul(inv, ya);
