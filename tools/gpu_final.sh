@@ -1,6 +1,7 @@
 # Round-end check: every GPU test, the default bench line (all configs, CPU baselines), the
 # shard-of-8 rehearsal, a rocprof kernel summary of the N=256 epoch and of the C4 round, and the
-# PMC passes of the one-lane share check.  Usage: gpurun -- bash tools/gpu_final.sh <tag>
+# PMC passes (wave states, FETCH_SIZE, WRITE_SIZE) with the traffic records of the one-lane share
+# check and the two-lane coin check.  Usage: COMMIT=<sha> gpurun -- bash tools/gpu_final.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -15,5 +16,12 @@ timeout -k 10 300 python -u bench.py --shard-of 8 --no-cpu-baseline --configs= >
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${tag}_prof" -o run -- python3 -u "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --in-flight 1 --configs=C4 > "$R/gpurun_out/${tag}_prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/${tag}_prof.log"; exit 1; }
 python3 "$R/tools/kstats.py" "$R/gpurun_out/${tag}_prof/run_results.db" > "$R/gpurun_out/${tag}_kernel_stats.txt" && head -30 "$R/gpurun_out/${tag}_kernel_stats.txt"
-cd "$R" && bash tools/gpu_pmc_fe.sh ${tag} 1 > /dev/null 2>&1 || echo "pmc failed"
+cd "$R" && bash tools/gpu_prof.sh ${tag}p > /dev/null 2>&1 || { echo "pmc failed"; exit 1; }
+# HBM-traffic records of the dominant regions (bench.py traffic_record): the one-lane share check
+# and the two-lane coin check, from the same FETCH / WRITE passes
+python3 tools/pmc_json.py gpurun_out/${tag}p_f/run_results.db gpurun_out/${tag}p_p/run_results.db \
+  "k_verify_shares_ml,k_fe1<0>,k_fe1<1>,k_fe1<3>,k_fe1<5>,k_verify_shares(" ${COMMIT:-unknown} > gpurun_out/${tag}_pmc_hbm.json || echo "pmc json failed"
+python3 tools/pmc_json.py gpurun_out/${tag}p_f/run_results.db gpurun_out/${tag}p_p/run_results.db \
+  "k_verify_sig_shares2(,k_verify_sig_shares2_fe<true>" ${COMMIT:-unknown} --skip-empty > gpurun_out/${tag}_pmc_coin.json || echo "pmc coin json failed"
+cat gpurun_out/${tag}_pmc_hbm.json gpurun_out/${tag}_pmc_coin.json
 echo done
