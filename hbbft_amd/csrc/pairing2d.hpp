@@ -870,6 +870,42 @@ __device__ __forceinline__ void line_dbl_step_2s(g2jd& T, bool l1, fq2d& c0, fq2
   T = g2jd{X3, Y3, Z3};
 }
 
+// pairingd.hpp line_add_step_di on the pair (T + Q with Q = (qx, qy) affine; both lanes hold T and
+// Q): 7 rounds instead of 14 products, inline -- the round-5 kernel called the one-lane step out of
+// line, through scratch frames (0.93 GB of scratch traffic per coin launch,
+// profiles/r06m_final_pmc_coin.json)
+__device__ __forceinline__ void line_add_step_2s(g2jd& T, const fq2d& qx, const fq2d& qy, bool l1, fq2d& c0,
+                                                 fq2d& c1, fq2d& c2) {
+  fq2d Z1Z1, qyZ, U2, S2, ZH, HH, nqx, ZpH2, r2, qyden, J, V, YJ, W;
+  round2_mul(l1, T.z, T.z, qy, T.z, Z1Z1, qyZ);
+  HBX_SEQ();
+  round2_mul(l1, qx, Z1Z1, qyZ, Z1Z1, U2, S2);
+  HBX_SEQ();
+  const fq2d H = fq2d_reduce(fq2d_sub(U2, T.x));
+  const fq2d num = fq2d_reduce(fq2d_sub(T.y, S2));
+  const fq2d r = fq2d_reduce(fq2d_dbl(fq2d_sub(S2, T.y)));
+  round2_mul(l1, T.z, H, H, H, ZH, HH);
+  HBX_SEQ();
+  const fq2d ZpH = fq2d_norm(fq2d_add(T.z, H));
+  round2_mul(l1, num, qx, ZpH, ZpH, nqx, ZpH2);
+  HBX_SEQ();
+  const fq2d den = fq2d_neg(ZH);
+  round2_mul(l1, r, r, qy, den, r2, qyden);
+  HBX_SEQ();
+  const fq2d I = fq2d_reduce(fq2d_dbl(fq2d_dbl(HH)));
+  c0 = fq2d_reduce(fq2d_sub(nqx, qyden));
+  c1 = fq2d_neg(num);
+  c2 = den;
+  const fq2d Z3 = fq2d_reduce(fq2d_sub(fq2d_sub(ZpH2, Z1Z1), HH));
+  round2_mul(l1, H, I, T.x, I, J, V);
+  HBX_SEQ();
+  const fq2d X3 = fq2d_reduce(fq2d_sub(fq2d_sub(r2, J), fq2d_dbl(V)));
+  round2_mul(l1, T.y, J, r, fq2d_sub(V, X3), YJ, W);
+  HBX_SEQ();
+  const fq2d Y3 = fq2d_reduce(fq2d_sub(W, fq2d_dbl(YJ)));
+  T = g2jd{X3, Y3, Z3};
+}
+
 // The coin check's two Miller loops on a pair with H''s prepared lines LH (68, Miller order; the
 // instance's, wave-uniform): lane 0 holds s = 1 / y_pk, lane 1 s = x_pk / y_pk (point_scalar2d of
 // pk_i); useH false: the H' pair contributes 1.  sigma (*q) at -[m] g1 = (px, py) in digit form;
@@ -902,8 +938,8 @@ __device__ __forceinline__ fq6d miller_gen2s(const line_pre_d* LH, const fqd& s,
     if (!add) {
       line_dbl_step_2s(T, l1, c0, c1, c2);
     } else {
-      const g2a Q = *q;  // both lanes run sigma's addition step (the same values)
-      line_add_step_call(T, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), c0, c1, c2);
+      const g2a Q = *q;  // sigma's addition step, split over the pair like the doubling
+      line_add_step_2s(T, fq2d_from_fq2(Q.x), fq2d_from_fq2(Q.y), l1, c0, c1, c2);
     }
     HBX_SEQ();
     // sigma's (c1 px | c2 py) and H''s scaled (h0 / y | h1 x / y), one product per lane each
