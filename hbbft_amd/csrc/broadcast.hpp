@@ -274,6 +274,9 @@ HBX_RS_INST(32, 4)
 HBX_RS_INST(64, 2)
 HBX_RS_INST(24, 4)
 HBX_RS_INST(48, 2)
+HBX_RS_INST(28, 2)
+HBX_RS_INST(28, 4)
+HBX_RS_INST(44, 2)
 #undef HBX_RS_INST
 #endif
 

@@ -286,26 +286,46 @@ static gf_ptab gf_perm_table(uint8_t c) {
   return t;
 }
 
-// Output rows x dwords per lane of the byte-permute kernel; HBX_RS_TILE (0..4) selects one of
-// the compiled variants for tuning.
+// Output rows x dwords per lane of the byte-permute kernel; HBX_RS_TILE (0..7) pins one of the
+// compiled variants for tuning, -1 (unset) picks by output count (rs_auto_tile).
 static int rs_tile() {
   static const int t = [] {
     const char* e = getenv("HBX_RS_TILE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
   return t;
 }
 
+static const int rs_tile_ch[] = {32, 32, 64, 24, 48, 28, 28, 44};
+
+// The tile whose row count wastes the fewest computed rows on `no` outputs per instance (each
+// pass over the k input rows yields CH outputs; a short last pass still reads all k rows), ties
+// to the larger tile.  r06q_rs_tiles: m = 84 parity rows run 740 GB/s on 32-row tiles (96 rows
+// computed) and 810 GB/s on 28-row ones (84).
+static int rs_auto_tile(uint32_t k, uint32_t no) {
+  static const int cand[] = {2, 4, 7, 0, 5, 3};  // 64, 48, 44, 32, 28, 24 rows, two dwords per lane but 24
+  int best = 3, best_rows = 1 << 30;
+  for (int t : cand) {
+    const int ch = rs_tile_ch[t];
+    if (rs_perm_lds_bytes(k, ch) > 65536) continue;
+    const int rows = (int)((no + ch - 1) / ch) * ch;
+    if (rows < best_rows) best = t, best_rows = rows;
+  }
+  return best;
+}
+
 // One coding pass: the byte-permute kernel when rows are whole dwords, else the LDS log/exp one.
+// `no` is the outputs one instance's pass is expected to write: m on encode; on a reconstruct pass
+// the f = m / 2 erasures of hbbft's fault bound (the bench's pattern; up to m still runs, in more passes).
 static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, uint32_t k, uint32_t inst,
-                    const rs_job* jobs, const uint16_t* coef, const gf_ptab* ptab, uint32_t job_stride, hipStream_t s) {
+                    const rs_job* jobs, const uint16_t* coef, const gf_ptab* ptab, uint32_t job_stride, uint32_t no,
+                    hipStream_t s) {
   timed t_(c, HBX_K_RS_CODE, s);
   if (L % 4 == 0) {
     const uint32_t Ld = L / 4;
-    static const int tile_ch[] = {32, 32, 64, 24, 48};
     int tile = rs_tile();
-    if (tile < 0 || tile > 4) tile = 0;
-    if (rs_perm_lds_bytes(k, tile_ch[tile]) > 65536) tile = 3;  // 24 x 128 x 20 B fits any k
+    if (tile < 0 || tile > 7) tile = rs_auto_tile(k, no);
+    if (rs_perm_lds_bytes(k, rs_tile_ch[tile]) > 65536) tile = 3;  // 24 x 128 x 20 B fits any k
     switch (tile) {
 #define HBX_RS_TILE(ch, d)                                                                                        \
   hipLaunchKernelGGL((k_rs_code_perm<ch, d>), dim3((Ld + 256 * d - 1) / (256 * d), inst), dim3(256),               \
@@ -315,6 +335,9 @@ static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, ui
       case 2: HBX_RS_TILE(64, 2)
       case 3: HBX_RS_TILE(24, 4)
       case 4: HBX_RS_TILE(48, 2)
+      case 5: HBX_RS_TILE(28, 2)
+      case 6: HBX_RS_TILE(28, 4)
+      case 7: HBX_RS_TILE(44, 2)
       default: HBX_RS_TILE(32, 2)
 #undef HBX_RS_TILE
     }
@@ -418,10 +441,10 @@ static int rs_reconstruct(hbx_ctx* c, uint8_t* d_shards, const uint8_t* d_presen
     HIPCHK(c, hipGetLastError());
   }
   rs_code(c, d_shards, stride, L, k, inst, c->rs_jobs_d.as<rs_job>(), c->rs_coef_d.as<uint16_t>(),
-          c->rs_ptab_d.as<gf_ptab>(), 1u, s);
+          c->rs_ptab_d.as<gf_ptab>(), 1u, (m + 1) / 2, s);
   HIPCHK(c, hipGetLastError());
   rs_code(c, d_shards, stride, L, k, inst, c->rs_jobs_p.as<rs_job>(), c->rs_coef_p.as<uint16_t>(),
-          c->rs_ptab_p.as<gf_ptab>(), 1u, s);
+          c->rs_ptab_p.as<gf_ptab>(), 1u, (m + 1) / 2, s);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
@@ -917,7 +940,7 @@ int hbx_rs_encode_d(hbx_ctx* c, uint8_t* d_shards, uint32_t inst, uint32_t k, ui
   int rc = rs_setup(c, k, m, s);
   if (rc) return rc;
   rs_code(c, d_shards, (size_t)(k + m) * L, L, k, inst, c->rs_enc_job.as<rs_job>(), c->rs_enc_coef.as<uint16_t>(),
-          c->rs_enc_ptab.as<gf_ptab>(), 0u, s);
+          c->rs_enc_ptab.as<gf_ptab>(), 0u, m, s);
   HIPCHK(c, hipGetLastError());
   return HBX_OK;
 }
