@@ -877,18 +877,19 @@ def config_c5(args, dev, torch, Context):
             if name == "sha256":
                 enc = ms["encode"]
                 dwords = inst * (L // 4)
-                enc_valu = dwords * m * k * 4.5  # 3 v_perm_b32 + 1.5 v_bitop3 per (out, in, dword)
+                enc_valu = dwords * m * k * 4.0  # k_rs_code_perm3: 8 v_perm_b32 + 4 v_bitop3 per (out, input triple, dword)
+                krs = "k_rs_code_perm3"
                 variants["rs_encode"] = {
                     "ms": round(enc, 4), "kernel_ms_per_launch": round(rs_ms / max(rs_cnt, 1), 4),
                     "roofline": {"bound": "valu (v_perm_b32 table lookups)", "achieved": round(rs_bytes / (enc * 1e-3) / 1e9, 1),
                                  "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(rs_bytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                  "valu_frac": round(enc_valu / (enc * 1e-3) / PEAK_VALU_OPS, 3),
                                  "valu_floor_ms": round(enc_valu / PEAK_VALU_OPS * 1e3, 3),
-                                 "traffic": pmc.get("k_rs_code_perm", {}).get("bytes_per_launch"),
+                                 "traffic": pmc.get(krs, {}).get("bytes_per_launch"),
                                  "traffic_note": ("PMC per launch averaged over the run's encode AND reconstruct "
-                                                  f"launches ({pmc['k_rs_code_perm']['launches'][0]}), "
-                                                  f"{pmc['k_rs_code_perm']['source']}" if "k_rs_code_perm" in pmc else None),
-                                 "kernel": "k_rs_code_perm",
+                                                  f"launches ({pmc[krs]['launches'][0]}), "
+                                                  f"{pmc[krs]['source']}" if krs in pmc else None),
+                                 "kernel": krs,
                                  "work": f"{inst} x ({k} L read + {m} L written), L = {L}"}}
     sub = {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} instances of a 1 MiB proposal (shard {L} B)",
            "value": variants["sha256"]["value"], "unit": variants["sha256"]["unit"],

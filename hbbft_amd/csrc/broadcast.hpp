@@ -169,6 +169,9 @@ __host__ __device__ constexpr size_t rs_perm_lds_bytes(uint32_t k, int ch) {
   return (size_t)((k + 1) & ~1u) * ch * 20;
 }
 
+#ifndef HBX_RS_LOADS
+#define HBX_RS_LOADS 0  // 1: branch-free clamped loads (r06s: 0.474 vs 0.467 ms on encode, kept off)
+#endif
 #if HBX_IN_TU(6)
 template <int CH, int D>
 __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
@@ -191,6 +194,18 @@ __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shar
   bool ok[D];
 #pragma unroll
   for (int j = 0; j < D; j++) ok[j] = wave0 + lane + 64 * j < Ld;
+#if HBX_RS_LOADS
+  // Branch-free loads: lanes past the row end read its last dword and inputs past k (the odd
+  // k's pad row) re-read row k - 1 -- their results are not stored / their tables are zero.
+  uint32_t off[D];
+#pragma unroll
+  for (int j = 0; j < D; j++) off[j] = min(wave0 + lane + 64 * j, Ld - 1);
+  auto load_in = [&](uint32_t c, uint32_t* d) {
+    const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c < k ? c : k - 1]) * Ld;
+#pragma unroll
+    for (int j = 0; j < D; j++) d[j] = src[off[j]];
+  };
+#else
   auto load_in = [&](uint32_t c, uint32_t* d) {
     if (c < k) {
       const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c]) * Ld + wave0 + lane;
@@ -201,7 +216,10 @@ __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shar
       for (int j = 0; j < D; j++) d[j] = 0u;
     }
   };
-  for (int o0 = 0; o0 < no; o0 += CH) {
+#endif
+  // passes of CH outputs spread over grid.z (host: ceil(expected outputs / CH)); more outputs
+  // than the grid covers loop here
+  for (int o0 = blockIdx.z * CH; o0 < no; o0 += gridDim.z * CH) {
     __syncthreads();  // previous pass done with the tables
     for (uint32_t e = threadIdx.x; e < kp * CH; e += blockDim.x) {
       const uint32_t c = e / CH, o = e % CH;
@@ -264,6 +282,132 @@ __global__ void __launch_bounds__(256) k_rs_code_perm(uint8_t* __restrict__ shar
   }
 }
 #endif
+
+// The same product over input TRIPLES: a byte's 8 bits split 3 + 3 + 2, and the two 2-bit tops
+// of a triple's three inputs (6 bits) are regrouped as two 3-bit lookups into mixed 8-entry
+// tables -- M1[a7 a6 | b6] = c_a (a_top << 6) ^ c_b (b6 << 6), M2[b7 | c7 c6] = c_b (b7 << 7) ^
+// c_c (c_top << 6) -- so a triple costs 8 v_perm + 4 v_bitop3 per output dword: 4.0 VALU ops per
+// coefficient and data dword against the pair kernel's 4.5 (which spends 3 perms on every
+// byte).  LDS per pass: [triple][CH] x 64 B ({T0,T1} of a, b, c; {M1, M2}), staged from the
+// per-coefficient gf_ptab tables; inputs past k (pad of the last triple) have zero tables.
+__host__ __device__ constexpr size_t rs_perm3_lds_bytes(uint32_t k, int ch) {
+  return (size_t)((k + 2) / 3) * ch * 64;
+}
+
+#if HBX_IN_TU(6)
+#ifndef HBX_RS3_WPE
+#define HBX_RS3_WPE 1  // tuning: minimum waves per EU of the triple kernel (__launch_bounds__'s second bound)
+#endif
+template <int CH, int D>
+__global__ void __launch_bounds__(256, HBX_RS3_WPE) k_rs_code_perm3(uint8_t* __restrict__ shards, size_t inst_stride, uint32_t L,
+                                                       uint32_t k, const rs_job* __restrict__ jobs,
+                                                       const gf_ptab* __restrict__ tables, uint32_t job_stride) {
+  extern __shared__ uint4 rs_lds[];
+  const uint32_t nt = (k + 2) / 3;
+  const uint32_t inst = blockIdx.y;
+  const rs_job* J = jobs + (size_t)inst * job_stride;
+  const int no = ld_uniform(&J->n_out);
+  if (no == 0) return;
+  const uint32_t Ld = L >> 2;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * D;
+  uint32_t* base = reinterpret_cast<uint32_t*>(shards + (size_t)inst * inst_stride);
+  const gf_ptab* tb = tables + (size_t)inst * job_stride * RS_MAX_N * k;
+  bool ok[D];
+#pragma unroll
+  for (int j = 0; j < D; j++) ok[j] = wave0 + lane + 64 * j < Ld;
+  auto load_in = [&](uint32_t c, uint32_t* d) {
+    if (c < k) {
+      const uint32_t* src = base + (size_t)ld_uniform(&J->in_idx[c]) * Ld + wave0 + lane;
+#pragma unroll
+      for (int j = 0; j < D; j++) d[j] = ok[j] ? src[64 * j] : 0u;
+    } else {
+#pragma unroll
+      for (int j = 0; j < D; j++) d[j] = 0u;
+    }
+  };
+  auto tbyte = [](uint32_t w, int i) { return (w >> (8 * i)) & 0xffu; };
+  // passes of CH outputs spread over grid.z (host: ceil(expected outputs / CH)); more outputs
+  // than the grid covers loop here
+  for (int o0 = blockIdx.z * CH; o0 < no; o0 += gridDim.z * CH) {
+    __syncthreads();  // previous pass done with the tables
+    for (uint32_t e = threadIdx.x; e < nt * CH; e += blockDim.x) {
+      const uint32_t t = e / CH, o = e % CH;
+      gf_ptab g[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const uint32_t c = 3 * t + i;
+        g[i] = gf_ptab{};
+        if (c < k && o0 + (int)o < no) g[i] = tb[(size_t)(o0 + o) * k + c];
+      }
+      // T2 (w[4]) byte i = c * (i << 6): byte 1 = c * 0x40, byte 2 = c * 0x80
+      uint32_t m1[2] = {0, 0}, m2[2] = {0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t v1 = tbyte(g[0].w[4], j & 3) ^ ((j & 4) ? tbyte(g[1].w[4], 1) : 0u);
+        const uint32_t v2 = ((j & 1) ? tbyte(g[1].w[4], 2) : 0u) ^ tbyte(g[2].w[4], j >> 1);
+        m1[j >> 2] |= v1 << (8 * (j & 3));
+        m2[j >> 2] |= v2 << (8 * (j & 3));
+      }
+      uint4* dst = rs_lds + (size_t)e * 4;
+      dst[0] = make_uint4(g[0].w[0], g[0].w[1], g[0].w[2], g[0].w[3]);
+      dst[1] = make_uint4(g[1].w[0], g[1].w[1], g[1].w[2], g[1].w[3]);
+      dst[2] = make_uint4(g[2].w[0], g[2].w[1], g[2].w[2], g[2].w[3]);
+      dst[3] = make_uint4(m1[0], m1[1], m2[0], m2[1]);
+    }
+    __syncthreads();
+    if (wave0 >= Ld) continue;  // a wave wholly past the row end only stages tables (uniform)
+    uint32_t acc[CH][D];
+#pragma unroll
+    for (int o = 0; o < CH; o++)
+#pragma unroll
+      for (int j = 0; j < D; j++) acc[o][j] = 0;
+    uint32_t na[D], nb[D], nc[D];
+    load_in(0, na);
+    load_in(1, nb);
+    load_in(2, nc);
+#pragma unroll 1
+    for (uint32_t t = 0; t < nt; t++) {
+      uint32_t a0[D], a1[D], b0[D], b1[D], c0[D], c1[D], s1[D], s2[D];
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        a0[j] = na[j] & 0x07070707u;
+        a1[j] = (na[j] >> 3) & 0x07070707u;
+        b0[j] = nb[j] & 0x07070707u;
+        b1[j] = (nb[j] >> 3) & 0x07070707u;
+        c0[j] = nc[j] & 0x07070707u;
+        c1[j] = (nc[j] >> 3) & 0x07070707u;
+        s1[j] = ((na[j] >> 6) & 0x03030303u) | ((nb[j] >> 4) & 0x04040404u);
+        s2[j] = ((nb[j] >> 7) & 0x01010101u) | ((nc[j] >> 5) & 0x06060606u);
+      }
+      load_in(3 * t + 3, na);
+      load_in(3 * t + 4, nb);
+      load_in(3 * t + 5, nc);
+      const uint4* tp = rs_lds + (size_t)t * CH * 4;
+#pragma unroll
+      for (int o = 0; o < CH; o++) {
+        const uint4 A = tp[4 * o], B = tp[4 * o + 1], C = tp[4 * o + 2], M = tp[4 * o + 3];
+#pragma unroll
+        for (int j = 0; j < D; j++) {
+          uint32_t x = xor3(acc[o][j], __builtin_amdgcn_perm(A.y, A.x, a0[j]), __builtin_amdgcn_perm(A.w, A.z, a1[j]));
+          x = xor3(x, __builtin_amdgcn_perm(B.y, B.x, b0[j]), __builtin_amdgcn_perm(B.w, B.z, b1[j]));
+          x = xor3(x, __builtin_amdgcn_perm(C.y, C.x, c0[j]), __builtin_amdgcn_perm(C.w, C.z, c1[j]));
+          acc[o][j] = xor3(x, __builtin_amdgcn_perm(M.y, M.x, s1[j]), __builtin_amdgcn_perm(M.w, M.z, s2[j]));
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CH; o++) {
+      if (o0 + o < no) {
+        uint32_t* dst = base + (size_t)ld_uniform(&J->out_idx[o0 + o]) * Ld + wave0 + lane;
+#pragma unroll
+        for (int j = 0; j < D; j++)
+          if (ok[j]) dst[64 * j] = acc[o][j];
+      }
+    }
+  }
+}
+#endif
 #if defined(HBX_TU) && HBX_TU == 6
 // the tiles rs_code() (hbx_api.hip) launches, instantiated in this translation unit
 #define HBX_RS_INST(ch, d)                                                                                   \
@@ -278,6 +422,17 @@ HBX_RS_INST(28, 2)
 HBX_RS_INST(28, 4)
 HBX_RS_INST(44, 2)
 #undef HBX_RS_INST
+#define HBX_RS_INST3(ch, d)                                                                                  \
+  template __global__ void k_rs_code_perm3<ch, d>(uint8_t* __restrict__, size_t, uint32_t, uint32_t,           \
+                                                   const rs_job* __restrict__, const gf_ptab* __restrict__, uint32_t);
+HBX_RS_INST3(24, 2)
+HBX_RS_INST3(28, 2)
+HBX_RS_INST3(32, 2)
+HBX_RS_INST3(42, 2)
+HBX_RS_INST3(24, 1)
+HBX_RS_INST3(28, 1)
+HBX_RS_INST3(42, 1)
+#undef HBX_RS_INST3
 #endif
 
 // reconstruct_shards set-up, one block per instance (reed-solomon-erasure 3.1.0):
@@ -666,8 +821,10 @@ __global__ void __launch_bounds__(128) k_merkle_leaves_sha256(const uint8_t* __r
         const uint32_t kv[4] = {k4.x, k4.y, k4.z, k4.w};
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          const uint32_t t1 = h + sha_sig(e, 6, 11, 25) + ((e & f) ^ (~e & g)) + kv[q];
-          const uint32_t t2 = sha_sig(a, 2, 13, 22) + ((a & bb) ^ (a & c) ^ (bb & c));
+          // Ch and Maj as one v_bitop3 each (truth tables 0xCA: e ? f : g, 0xE8: majority); the
+          // compiler's own Maj took three ops (14 VALU per round instead of 16)
+          const uint32_t t1 = h + kv[q] + sha_sig(e, 6, 11, 25) + __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+          const uint32_t t2 = sha_sig(a, 2, 13, 22) + __builtin_amdgcn_bitop3_b32(a, bb, c, 0xE8);
           h = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + t2;
         }
       }

@@ -296,6 +296,15 @@ static int rs_tile() {
   return t;
 }
 
+// HBX_RS_K3=0 keeps the pair kernel (k_rs_code_perm) where the triple one would run.
+static bool rs_k3() {
+  static const bool t = [] {
+    const char* e = getenv("HBX_RS_K3");
+    return !e || atoi(e) != 0;
+  }();
+  return t;
+}
+
 static const int rs_tile_ch[] = {32, 32, 64, 24, 48, 28, 28, 44};
 
 // The tile whose row count wastes the fewest computed rows on `no` outputs per instance (each
@@ -321,6 +330,41 @@ static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, ui
                     const rs_job* jobs, const uint16_t* coef, const gf_ptab* ptab, uint32_t job_stride, uint32_t no,
                     hipStream_t s) {
   timed t_(c, HBX_K_RS_CODE, s);
+  if (no == 0) no = 1;  // grid.z >= 1; the kernels read the true count from the job
+  if (L % 4 == 0 && rs_k3() && rs_tile() < 0) {
+    // triple kernel (4.0 VALU ops per coefficient-dword): tile by output count as below
+    const uint32_t Ld = L / 4;
+    static const int ch3[] = {28, 42, 32, 24};  // ties to the first: 28 rows run 105 VGPRs, 42 run 130
+    int ch = 0, best_rows = 1 << 30;
+    for (int t : ch3) {
+      if (rs_perm3_lds_bytes(k, t) > 65536) continue;
+      const int rows = (int)((no + t - 1) / t) * t;
+      if (rows < best_rows) ch = t, best_rows = rows;
+    }
+    static const int pin = [] {
+      const char* e = getenv("HBX_RS_CH3");  // tuning: 100 * D + CH of a compiled triple tile
+      return e ? atoi(e) : 0;
+    }();
+    int d3 = 2;
+    if (pin && rs_perm3_lds_bytes(k, pin % 100) <= 65536) ch = pin % 100, d3 = pin / 100;
+    if (ch) {
+      switch (d3 * 100 + ch) {
+#define HBX_RS_TILE3(c3, d)                                                                                         \
+  hipLaunchKernelGGL((k_rs_code_perm3<c3, d>), dim3((Ld + 256 * d - 1) / (256 * d), inst, (no + c3 - 1) / c3), dim3(256), \
+                     rs_perm3_lds_bytes(k, c3), s, d_shards, stride, L, k, jobs, ptab, job_stride);                  \
+  break;
+        case 242: HBX_RS_TILE3(42, 2)
+        case 232: HBX_RS_TILE3(32, 2)
+        case 228: HBX_RS_TILE3(28, 2)
+        case 142: HBX_RS_TILE3(42, 1)
+        case 128: HBX_RS_TILE3(28, 1)
+        case 124: HBX_RS_TILE3(24, 1)
+        default: HBX_RS_TILE3(24, 2)
+#undef HBX_RS_TILE3
+      }
+      return;
+    }
+  }
   if (L % 4 == 0) {
     const uint32_t Ld = L / 4;
     int tile = rs_tile();
@@ -328,7 +372,7 @@ static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, ui
     if (rs_perm_lds_bytes(k, rs_tile_ch[tile]) > 65536) tile = 3;  // 24 x 128 x 20 B fits any k
     switch (tile) {
 #define HBX_RS_TILE(ch, d)                                                                                        \
-  hipLaunchKernelGGL((k_rs_code_perm<ch, d>), dim3((Ld + 256 * d - 1) / (256 * d), inst), dim3(256),               \
+  hipLaunchKernelGGL((k_rs_code_perm<ch, d>), dim3((Ld + 256 * d - 1) / (256 * d), inst, (no + ch - 1) / ch), dim3(256), \
                      rs_perm_lds_bytes(k, ch), s, d_shards, stride, L, k, jobs, ptab, job_stride);                 \
   break;
       case 1: HBX_RS_TILE(32, 4)

@@ -23,7 +23,10 @@ def dev(a):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,L,inst", [(2, 2, 5, 3), (3, 4, 37, 2), (5, 8, 64, 4), (44, 84, 1000, 2), (86, 170, 33, 1),
                                           (1, 1, 4, 2), (2, 3, 8, 3), (86, 170, 516, 1), (44, 84, 23832, 2),
-                                          (128, 128, 2052, 1), (3, 250, 4100, 1)])
+                                          (128, 128, 2052, 1), (3, 250, 4100, 1),
+                                          # input-triple kernel: k % 3 = 1 and 0 with several triples, a
+                                          # ragged last wave, more outputs than one tile
+                                          (7, 9, 64, 2), (9, 12, 1024, 2), (43, 86, 4100, 1), (42, 100, 2052, 2)])
 def test_rs_encode(hbx_ctx, k, m, L, inst):
     rng = np.random.default_rng(k * 1000 + L)
     data = np.zeros((inst, k + m, L), dtype=np.uint8)
@@ -39,7 +42,7 @@ def test_rs_encode(hbx_ctx, k, m, L, inst):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,L", [(2, 2, 9), (3, 4, 37), (44, 84, 257), (2, 2, 12), (44, 84, 1000), (44, 84, 23832),
-                                   (86, 170, 2052)])
+                                   (86, 170, 2052), (43, 86, 1024), (9, 12, 64)])
 def test_rs_reconstruct(hbx_ctx, k, m, L):
     n = k + m
     rs = rm.ReedSolomon(k, m)
