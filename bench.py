@@ -853,7 +853,27 @@ def config_c5(args, dev, torch, Context):
             assert (status.cpu().numpy() == 0).all(), "decode status"
             assert (out_len.cpu().numpy() == plen).all()
             assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "decoded payload"
+            # the same decode with the f erasures spread over data and parity shards (about a third
+            # of them data shards: the reconstruct solves for those), beside the parity-only pattern
+            spread = np.unique(np.linspace(0, n - 1, f).round().astype(np.int64))
+            present_mix = torch.ones((inst, n), dtype=torch.uint8, device=dev)
+            present_mix[:, torch.from_numpy(spread).to(dev)] = 0
+            mix_ms = []
+            for s in range(steps + 1):
+                work.copy_(shards)
+                work[present_mix == 0] = 0xA5
+                ev[3].record(stream)
+                ctx.broadcast_decode_d(work, present_mix, roots, k, m, out, out_len, status, stream=sh)
+                ev[4].record(stream)
+                torch.cuda.synchronize(dev)
+                if s:
+                    mix_ms.append(ev[3].elapsed_time(ev[4]))
+            assert (status.cpu().numpy() == 0).all(), "decode status (spread erasures)"
+            assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "decoded payload (spread erasures)"
+            res["decode_spread"] = mix_ms
+            res["erased_data_spread"] = [int((spread < k).sum())]
             roots_by[name] = roots.cpu().numpy().copy()
+            erased_data = res.pop("erased_data_spread")[0]
             ms = {key: float(np.mean(v)) for key, v in res.items()}
             leaf_bytes = inst * n * (L + 1)
             pmc = c5_traffic()
@@ -864,6 +884,8 @@ def config_c5(args, dev, torch, Context):
                 "value": round(inst * plen / (ms["step"] * 1e-3) / 1e9, 2),
                 "unit": "GB/s of proposals (encode + Merkle roots + decode with 42 missing)",
                 "ms": {key: round(v, 3) for key, v in ms.items()},
+                "decode_spread_note": (f"decode_spread: the {f} erasures at evenly spaced shard indices, {erased_data} of them "
+                                       f"data shards (decode: the last {f}, parity only); not in the step"),
                 "merkle_leaves_kernel_ms": round(ml, 4),
                 "merkle_leaves_GBps": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),
                 "roofline": {"bound": "hbm", "achieved": round(leaf_bytes / (ml * 1e-3) / 1e9, 1),

@@ -455,26 +455,34 @@ __global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __r
   __shared__ int32_t s_count, s_nmd, s_nmp, s_swap;
   __shared__ int32_t missing_data[RS_MAX_K], missing_par[RS_MAX_N];
   __shared__ uint8_t factor[RS_MAX_K];
+  __shared__ int32_t wcnt[4][3];
   gf_stage(T, glog, gexp);
   const uint32_t inst = blockIdx.x;
   const uint32_t n = k + m;
   const uint8_t* pr = present + (size_t)inst * n;
   const int tid = threadIdx.x;
+  // classification by ballots (n <= RS_MAX_N = blockDim): the rank of each shard among the
+  // present / missing-data / missing-parity ones, in index order
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const bool in = (uint32_t)tid < n, p = in && pr[tid] != 0;
+  const bool md = in && !p && (uint32_t)tid < k, mp = in && !p && (uint32_t)tid >= k;
+  const uint64_t bp = __ballot(p), bd = __ballot(md), bm = __ballot(mp);
+  const uint64_t below = (1ull << lane) - 1;
+  if (lane == 0) {
+    wcnt[wv][0] = __popcll(bp);
+    wcnt[wv][1] = __popcll(bd);
+    wcnt[wv][2] = __popcll(bm);
+  }
+  __syncthreads();
+  int op = 0, od = 0, om = 0;
+  for (uint32_t w = 0; w < wv; w++) op += wcnt[w][0], od += wcnt[w][1], om += wcnt[w][2];
+  if (p && op + __popcll(bp & below) < (int)k) sub[op + __popcll(bp & below)] = tid;
+  if (md) missing_data[od + __popcll(bd & below)] = tid;
+  if (mp) missing_par[om + __popcll(bm & below)] = tid;
   if (tid == 0) {
-    int c = 0, nmd = 0, nmp = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      if (pr[i]) {
-        if (c < (int)k) sub[c] = (int32_t)i;
-        c++;
-      } else if (i < k) {
-        missing_data[nmd++] = (int32_t)i;
-      } else {
-        missing_par[nmp++] = (int32_t)i;
-      }
-    }
-    s_count = c;
-    s_nmd = nmd;
-    s_nmp = nmp;
+    s_count = wcnt[0][0] + wcnt[1][0] + wcnt[2][0] + wcnt[3][0];
+    s_nmd = wcnt[0][1] + wcnt[1][1] + wcnt[2][1] + wcnt[3][1];
+    s_nmp = wcnt[0][2] + wcnt[1][2] + wcnt[2][2] + wcnt[3][2];
   }
   __syncthreads();
   rs_job& JD = jobs_data[inst];
@@ -487,41 +495,49 @@ __global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __r
     }
     return;
   }
-  // [sub-matrix | I]
-  for (uint32_t e = tid; e < k * 2 * k; e += blockDim.x) {
-    const uint32_t r = e / (2 * k), c = e % (2 * k);
-    A[r][c] = c < k ? enc[(size_t)sub[r] * k + c] : (c - k == r ? 1 : 0);
-  }
-  __syncthreads();
-  for (uint32_t r = 0; r < k; r++) {
-    if (tid == 0) {
-      s_swap = -1;
-      if (A[r][r] == 0)
-        for (uint32_t b = r + 1; b < k; b++)
-          if (A[b][r]) {
-            s_swap = (int32_t)b;
-            break;
-          }
+  // The sub-matrix of the first k present rows is [[I, 0], [E_p, E_m]] with the present data
+  // shards first (sub[0, npd)) and the first nmd present parity shards after them, columns as
+  // (present data D_p, missing data D_m).  Only its rows for D_m are needed:
+  //   x_m = E_m^-1 y_s + (E_m^-1 E_p) x_p,
+  // so Gauss-Jordan runs on the nmd x nmd block E_m (nmd = missing data shards; none when only
+  // parity is missing) instead of the whole k x k matrix -- the same unique coefficients.
+  const int nmd = s_nmd, npd = (int)k - nmd;
+  if (nmd > 0) {
+    for (uint32_t e = tid; e < (uint32_t)(nmd * 2 * nmd); e += blockDim.x) {  // [E_m | I]
+      const int r = (int)e / (2 * nmd), c = (int)e % (2 * nmd);
+      A[r][c] = c < nmd ? enc[(size_t)sub[npd + r] * k + missing_data[c]] : (c - nmd == r ? 1 : 0);
     }
     __syncthreads();
-    if (s_swap >= 0)
-      for (uint32_t c = tid; c < 2 * k; c += blockDim.x) {
-        const uint8_t t = A[r][c];
-        A[r][c] = A[s_swap][c];
-        A[s_swap][c] = t;
+    for (int r = 0; r < nmd; r++) {
+      if (tid == 0) {
+        s_swap = -1;
+        if (A[r][r] == 0)
+          for (int b2 = r + 1; b2 < nmd; b2++)
+            if (A[b2][r]) {
+              s_swap = b2;
+              break;
+            }
       }
-    __syncthreads();
-    const uint8_t piv = A[r][r];
-    const uint8_t inv = piv ? T.ex[255 - T.lg[piv]] : 0;  // MDS: piv != 0 after the row swap
-    __syncthreads();
-    for (uint32_t c = tid; c < 2 * k; c += blockDim.x) A[r][c] = gf_mul(T, A[r][c], inv);
-    for (uint32_t i = tid; i < k; i += blockDim.x) factor[i] = A[i][r];
-    __syncthreads();
-    for (uint32_t e = tid; e < k * 2 * k; e += blockDim.x) {
-      const uint32_t i = e / (2 * k), c = e % (2 * k);
-      if (i != r && factor[i]) A[i][c] ^= gf_mul(T, factor[i], A[r][c]);
+      __syncthreads();
+      if (s_swap >= 0)
+        for (int c = tid; c < 2 * nmd; c += blockDim.x) {
+          const uint8_t t = A[r][c];
+          A[r][c] = A[s_swap][c];
+          A[s_swap][c] = t;
+        }
+      __syncthreads();
+      const uint8_t piv = A[r][r];
+      const uint8_t inv = piv ? T.ex[255 - T.lg[piv]] : 0;  // MDS: E_m is invertible
+      __syncthreads();
+      for (int c = tid; c < 2 * nmd; c += blockDim.x) A[r][c] = gf_mul(T, A[r][c], inv);
+      for (int i = tid; i < nmd; i += blockDim.x) factor[i] = A[i][r];
+      __syncthreads();
+      for (uint32_t e = tid; e < (uint32_t)(nmd * 2 * nmd); e += blockDim.x) {
+        const int i = (int)e / (2 * nmd), c = (int)e % (2 * nmd);
+        if (i != r && factor[i]) A[i][c] ^= gf_mul(T, factor[i], A[r][c]);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   // job 0: missing data rows from the k sub shards
   if (tid == 0) {
@@ -537,8 +553,14 @@ __global__ void __launch_bounds__(256) k_rs_setup_reconstruct(const uint8_t* __r
   for (int o = tid; o < s_nmp; o += blockDim.x) JP.out_idx[o] = missing_par[o];
   uint16_t* cd = coef_data + (size_t)inst * RS_MAX_N * k;
   for (uint32_t e = tid; e < (uint32_t)s_nmd * k; e += blockDim.x) {
-    const uint32_t o = e / k, c = e % k;
-    const uint8_t v = A[missing_data[o]][k + c];
+    const int o = (int)(e / k), c = (int)(e % k);
+    uint8_t v;
+    if (c >= npd) {
+      v = A[o][nmd + (c - npd)];  // E_m^-1 on the present parity shards
+    } else {                      // (E_m^-1 E_p) on the present data shards
+      v = 0;
+      for (int r = 0; r < nmd; r++) v ^= gf_mul(T, A[o][nmd + r], enc[(size_t)sub[npd + r] * k + sub[c]]);
+    }
     cd[o * k + c] = v ? T.lg[v] : GF_COEF_ZERO;
   }
   uint16_t* cp = coef_par + (size_t)inst * RS_MAX_N * k;
