@@ -961,7 +961,7 @@ __device__ __forceinline__ void keccak_f1600_il(uint32_t* a, uint32_t h) {
   for (int r = 0; r < 24; r++) {
     uint32_t c[5], rc1[5], b[25];
 #pragma unroll
-    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; x++) c[x] = xor3(xor3(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
     // rotl64(C, 1): the even half is the odd half rotated by 1, the odd half is the even half
 #pragma unroll
     for (int x = 0; x < 5; x++) {
@@ -969,11 +969,9 @@ __device__ __forceinline__ void keccak_f1600_il(uint32_t* a, uint32_t h) {
       rc1[x] = __builtin_amdgcn_alignbit(p, p, 31u + h);  // rotl by 1 - h
     }
 #pragma unroll
-    for (int x = 0; x < 5; x++) {
-      const uint32_t d = c[(x + 4) % 5] ^ rc1[(x + 1) % 5];
+    for (int x = 0; x < 5; x++)  // a ^= D[x] = C[x - 1] ^ rotl(C[x + 1], 1), one v_bitop3 per word
 #pragma unroll
-      for (int y = 0; y < 5; y++) a[5 * y + x] ^= d;
-    }
+      for (int y = 0; y < 5; y++) a[5 * y + x] = xor3(a[5 * y + x], c[(x + 4) % 5], rc1[(x + 1) % 5]);
     // rho + pi: b[pi(i)] = rotl64(a[i], RHO[i])
 #pragma unroll
     for (int x = 0; x < 5; x++)
