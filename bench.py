@@ -70,7 +70,7 @@ PEAK_TMAD_S = float(os.environ.get("HBX_PEAK_TMAD_S", "27.27"))
 PEAK_VALU_OPS = 256 * 4 * 16 * 2.4e9
 HBM_PEAK_GBPS = 8000.0
 # HBM traffic of one share-check launch at N=256, from a PMC pass (rocprofv3 --pmc FETCH_SIZE and
-# WRITE_SIZE in separate passes, tools/gpu_round.sh PMC=1): the newest profiles/*_pmc_hbm.json
+# WRITE_SIZE in separate passes, tools/gpu_final.sh via tools/gpu_prof.sh): the newest profiles/*_pmc_hbm.json
 # carries the kernel, the bytes per launch and the commit the pass was taken at.
 OWN_INDEX = 0  # the benchmarked node is validator 0 (own share computed locally, hbx_set_own_share)
 
