@@ -31,6 +31,29 @@ HBX_CONST uint32_t SHA256_K[64] = {
 
 HBX_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 HBX_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+// SHA-2 Ch / Maj and a three-way XOR: one v_bitop3_b32 each on the device (truth tables 0xCA,
+// 0xE8, 0x96; the compiler builds Maj from three ops), plain logic in the host build
+HBX_HD uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+#else
+  return (e & f) ^ (~e & g);
+#endif
+}
+HBX_HD uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
+HBX_HD uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 
 struct sha256_state {
   uint32_t h[8];
@@ -54,16 +77,16 @@ HBX_HDNI void sha256_compress(sha256_state& s, const uint32_t* w16) {
       wi = w[i];
     } else {
       const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = sha_xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = sha_xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
       w[i & 15] = wi;
     }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t S1 = sha_xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t ch = sha_ch(e, f, g);
+    const uint32_t t1 = h + SHA256_K[i] + wi + S1 + ch;
+    const uint32_t S0 = sha_xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t mj = sha_maj(a, b, c);
     const uint32_t t2 = S0 + mj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
