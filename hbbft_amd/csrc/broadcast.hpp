@@ -425,13 +425,11 @@ HBX_RS_INST(44, 2)
 #define HBX_RS_INST3(ch, d)                                                                                  \
   template __global__ void k_rs_code_perm3<ch, d>(uint8_t* __restrict__, size_t, uint32_t, uint32_t,           \
                                                    const rs_job* __restrict__, const gf_ptab* __restrict__, uint32_t);
-HBX_RS_INST3(24, 2)
+HBX_RS_INST3(12, 2)
+HBX_RS_INST3(14, 2)
+HBX_RS_INST3(21, 2)
 HBX_RS_INST3(28, 2)
-HBX_RS_INST3(32, 2)
 HBX_RS_INST3(42, 2)
-HBX_RS_INST3(24, 1)
-HBX_RS_INST3(28, 1)
-HBX_RS_INST3(42, 1)
 #undef HBX_RS_INST3
 #endif
 

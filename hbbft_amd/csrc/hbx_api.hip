@@ -334,7 +334,10 @@ static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, ui
   if (L % 4 == 0 && rs_k3() && rs_tile() < 0) {
     // triple kernel (4.0 VALU ops per coefficient-dword): tile by output count as below
     const uint32_t Ld = L / 4;
-    static const int ch3[] = {28, 42, 32, 24};  // ties to the first: 28 rows run 105 VGPRs, 42 run 130
+    // fewest computed rows, ties to the earlier entry: the 21-row tile runs 88 VGPRs (5 waves per
+    // SIMD) against 105 for 28 rows and 130 for 42 (r06t21: encode 0.405 -> 0.387-0.398 ms, the
+    // decode with spread erasures 1.33 -> 1.22 ms)
+    static const int ch3[] = {21, 14, 12, 28, 42};
     int ch = 0, best_rows = 1 << 30;
     for (int t : ch3) {
       if (rs_perm3_lds_bytes(k, t) > 65536) continue;
@@ -354,12 +357,10 @@ static void rs_code(hbx_ctx* c, uint8_t* d_shards, size_t stride, uint32_t L, ui
                      rs_perm3_lds_bytes(k, c3), s, d_shards, stride, L, k, jobs, ptab, job_stride);                  \
   break;
         case 242: HBX_RS_TILE3(42, 2)
-        case 232: HBX_RS_TILE3(32, 2)
         case 228: HBX_RS_TILE3(28, 2)
-        case 142: HBX_RS_TILE3(42, 1)
-        case 128: HBX_RS_TILE3(28, 1)
-        case 124: HBX_RS_TILE3(24, 1)
-        default: HBX_RS_TILE3(24, 2)
+        case 214: HBX_RS_TILE3(14, 2)
+        case 212: HBX_RS_TILE3(12, 2)
+        default: HBX_RS_TILE3(21, 2)
 #undef HBX_RS_TILE3
       }
       return;
