@@ -683,12 +683,12 @@ __device__ void sha256_node(const uint32_t* l8, const uint32_t* r8, uint32_t* ou
   w[8] = (l8[7] << 24) | (r8[0] >> 8);
 #pragma unroll
   for (int i = 9; i < 16; i++) w[i] = (r8[i - 9] << 24) | (r8[i - 8] >> 8);
-  sha256_compress(s, w);
+  sha256_compress_il(s, w);
   w[0] = (r8[7] << 24) | 0x00800000u;
 #pragma unroll
   for (int i = 1; i < 15; i++) w[i] = 0;
   w[15] = 65 * 8;
-  sha256_compress(s, w);
+  sha256_compress_il(s, w);
 #pragma unroll
   for (int i = 0; i < 8; i++) out8[i] = s.h[i];
 }

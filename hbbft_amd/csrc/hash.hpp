@@ -64,8 +64,9 @@ HBX_HD void sha256_init(sha256_state& s) {
   s.h[4] = 0x510e527fu; s.h[5] = 0x9b05688cu; s.h[6] = 0x1f83d9abu; s.h[7] = 0x5be0cd19u;
 }
 
-// One compression over 16 big-endian message words.
-HBX_HDNI void sha256_compress(sha256_state& s, const uint32_t* w16) {
+// One compression over 16 big-endian message words (inlined form: the Merkle node hash, whose
+// second block is constant but for one word, folds its schedule; sha256_compress is the call).
+HBX_HD void sha256_compress_il(sha256_state& s, const uint32_t* w16) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) w[i] = w16[i];
@@ -93,6 +94,7 @@ HBX_HDNI void sha256_compress(sha256_state& s, const uint32_t* w16) {
   s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
   s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
+HBX_HDNI void sha256_compress(sha256_state& s, const uint32_t* w16) { sha256_compress_il(s, w16); }
 
 // Streaming SHA-256 over a concatenation of up to two byte ranges (enough for hash_g1_g2's
 // "message || compress(g1)"), one lane.  Output: 32-byte digest.
