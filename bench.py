@@ -916,9 +916,59 @@ def config_c5(args, dev, torch, Context):
     sub = {"workload": f"Broadcast N={n} RS({k},{m}) x {inst} instances of a 1 MiB proposal (shard {L} B)",
            "value": variants["sha256"]["value"], "unit": variants["sha256"]["unit"],
            "merkle_sha256": variants["sha256"], "merkle_sha3": variants["sha3"], "rs_encode": variants["rs_encode"]}
+    if args.in_flight > 1:
+        sub["steps_in_flight"] = c5_in_flight(args, dev, torch, Context, shards, present, k, m, f, plen, payload, steps)
     if not args.no_cpu_baseline:
         sub["cpu_baseline"] = cpu_baseline_broadcast(host, k, m, L, payload, roots_by, args.cpu_seconds)
     return sub
+
+
+def c5_in_flight(args, dev, torch, Context, shards0, present, k, m, f, plen, payload, steps):
+    """C5 steps (encode + roots + decode, SHA-256 tree) with `args.in_flight` steps overlapping:
+    step s on context s mod F with its own shard, work and output buffers and stream, issued back
+    to back -- the leaf hashing's serial chains fill a quarter of the SIMDs, so the next batch of
+    proposals' coding and hashing run beside it (Broadcast instances of later epochs).  The
+    headline stays one step at a time."""
+    from hbbft_amd.hbx import MERKLE_SHA256
+
+    F = args.in_flight
+    inst, n, L = shards0.shape
+    lanes = []
+    for _ in range(F):
+        c = Context(dev.index or 0)
+        c.set_merkle_digest(MERKLE_SHA256)
+        st = torch.cuda.Stream(dev)
+        bufs = (shards0.clone(), torch.empty_like(shards0), torch.zeros((inst, 32), dtype=torch.uint8, device=dev),
+                torch.zeros((inst, k * L), dtype=torch.uint8, device=dev), torch.zeros(inst, dtype=torch.int64, device=dev),
+                torch.zeros(inst, dtype=torch.int32, device=dev))
+        lanes.append((c, st, bufs))
+    torch.cuda.synchronize(dev)
+
+    def issue(q):
+        c, st, (sh_, work, roots, out, out_len, status) = lanes[q % F]
+        with torch.cuda.stream(st):
+            c.rs_encode_d(sh_, k, m, stream=st.cuda_stream)
+            c.merkle_roots_d(sh_, roots, stream=st.cuda_stream)
+            work.copy_(sh_)
+            work[:, n - f:] = 0xA5
+            c.broadcast_decode_d(work, present, roots, k, m, out, out_len, status, stream=st.cuda_stream)
+
+    for q in range(F):
+        issue(q)
+    torch.cuda.synchronize(dev)
+    total = F * max(steps, 2)
+    t0 = time.perf_counter()
+    for q in range(total):
+        issue(q)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    for c, _, (_, _, _, out, out_len, status) in lanes:
+        assert (status.cpu().numpy() == 0).all() and (out_len.cpu().numpy() == plen).all(), "in-flight decode status"
+        assert np.array_equal(out[:, :plen].cpu().numpy(), payload), "in-flight decoded payload"
+        c.close()
+    return {"steps": total, "in_flight": F, "ms_per_step": round(elapsed / total * 1e3, 3),
+            "value": round(inst * plen * total / elapsed / 1e9, 2),
+            "unit": "GB/s of proposals (wall clock, steps overlapping; SHA-256 tree)"}
 
 
 def echo_epoch(ctx, torch, dev, stream, shards, roots, present, k, m, steps):
