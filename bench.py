@@ -562,6 +562,8 @@ def config_c2(args, dev, torch, Context):
         kern = eb.kernel_ms()
         ctx.set_timing(False)
         lanes = ctx.verify_lanes_used()
+        # latency-bound at N=64: the node's rate with epochs overlapping (HoneyBadger's future epochs)
+        flight = in_flight(args, eb, dev, torch, Context, n * n) if args.in_flight > 1 else None
     ms = elapsed / steps * 1e3
     res = {"workload": f"HoneyBadger node-epoch N={n}: {n * n} decryption-share verifies + {n} Ciphertext::verify + "
                        f"{n} combines (t={ep['t']}) + decrypt, |v|={args.vlen} B",
@@ -572,6 +574,8 @@ def config_c2(args, dev, torch, Context):
            "roofline": verify_roofline(n * n, kern["verify_shares"], f"k_verify_shares{lanes if lanes > 1 else ''} "
                                        "(auto: 64 x 64 checks fill 1/16 of the chip one lane per check)"),
            "note": "latency-bound: 4,096 checks leave most SIMDs idle; the per-proposer chains set the time"}
+    if flight:
+        res["epochs_in_flight"] = flight
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_dec(ep, args.cpu_seconds)
     return res
