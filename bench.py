@@ -496,12 +496,15 @@ def config_c1(args, dev, torch, Context):
             torch.cuda.synchronize(dev)
             wall.append(time.perf_counter() - t0)
         eb.check(0)
+        flight = in_flight(args, eb, dev, torch, Context, n * n) if args.in_flight > 1 else None
     res = {"workload": f"node-epoch crypto at N={n} (simulation example's 10 nodes): {n} Ciphertext::verify + "
                        f"{n * (n - 1)} decryption-share verifies + {n} combines (t={ep['t']}) + decrypt, |v|={args.vlen} B",
            "value": round(1e3 * float(np.mean(wall)), 3), "unit": "ms per node-epoch (wall, one call, synchronised)",
            "higher_is_better": False,
            "epoch_ms_hip_events": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), 3),
            "note": "latency-bound: 100 checks occupy 100 lanes; the chain of dependent stages sets the time"}
+    if flight:
+        res["epochs_in_flight"] = flight
     if not args.no_cpu_baseline:
         lib = cpu_lib()
         cts = ep["cts"]
