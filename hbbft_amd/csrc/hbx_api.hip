@@ -908,8 +908,8 @@ static int verify_impl(hbx_ctx* c, const uint8_t* d_shares, const uint8_t* d_pre
                          own ? c->own_me : UINT32_MAX,
                          (own && !c->ct_known) ? c->ct_valid.as<uint8_t>() : nullptr, 0u, nullptr);
     else {
-      // one lane per check: the Miller loops, then the final exponentiation as seven step kernels
-      // over per-lane slots (fe1d.hpp: no Fq12 ever crosses a call frame)
+      // one lane per check: the Miller loops, then the final exponentiation's seven steps as four
+      // kernels over per-lane slots (fe1d.hpp: no Fq12 ever crosses a call frame)
       const dim3 grid((n + 63) / 64, p);
       if (!c->fe1slot.ensure((size_t)grid.x * grid.y * 64 * 3 * FE1_WORDS * 4))
         return fail(c, HBX_E_OUT_OF_MEMORY, "hbx_verify_dec_shares_d: out of device memory (slots)");

@@ -362,8 +362,8 @@ __global__ void __launch_bounds__(64) k_verify_shares(const g1a* __restrict__ S,
 }
 
 // One lane per share, the Miller loop only (k_verify_shares up to its final exponentiation): the
-// Miller value conj(f) goes to the lane's global slot F (fe1d.hpp) for the seven k_fe1 steps, the
-// share status byte is final unless it is SHARE_PENDING (k_fe1<6> decides those).
+// Miller value conj(f) goes to the lane's global slot F (fe1d.hpp) for the four k_fe1 kernels, the
+// share status byte is final unless it is SHARE_PENDING (k_fe1<5> decides those).
 __global__ void __launch_bounds__(64) k_verify_shares_ml(const g1a* __restrict__ S, const int32_t* __restrict__ s_status,
                                                          const uint8_t* __restrict__ present,
                                                          const g1a* __restrict__ pk, uint32_t n_keys,
@@ -440,9 +440,10 @@ __global__ void __launch_bounds__(64, HBX_V3_WAVES) k_verify_shares3(const g1a* 
 #endif
 
 #if HBX_IN_TU(8) || HBX_IN_TU(9) || HBX_IN_TU(10)
-// The seven final-exponentiation steps of the one-lane share checks (fe1d.hpp), over the same grid
-// as k_verify_shares_ml (lane = sender i, blockIdx.y = proposer j).  Lanes whose status is not
-// SHARE_PENDING have nothing to do.  Step 6 turns SHARE_PENDING into HBX_SHARE_VALID / INVALID and,
+// The final-exponentiation steps F0..F6 of the one-lane share checks (fe1d.hpp) as four kernels
+// (k_fe1<0>, <1>, <3>, <5>), over the same grid as k_verify_shares_ml (lane = sender i, blockIdx.y =
+// proposer j).  Lanes whose status is not SHARE_PENDING have nothing to do.  The last kernel (F5 +
+// F6) turns SHARE_PENDING into HBX_SHARE_VALID / INVALID and,
 // in own-share mode, writes the own lane's verdict as Ciphertext::verify (k_verify_shares).
 #ifndef HBX_FE1_LANE_LDS
 #define HBX_FE1_LANE_LDS 0
